@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the batched CTR-Reach step on MI355X.
+
+Workload (BASELINE.json configs[2], the headline): 65 536 parallel 3-tube envs per GPU,
+torsionally-compliant model, scipy-faithful RK45 (parity mode, fp64), default CTR-Reach-v0
+kwargs (system 0, n_substeps 10, tol 0.020 m, max 150 steps), synthetic uniform actions,
+auto-resets at their natural rate inside the timed region.  A "step" = one batched
+CtrReachVecEnv.step over all envs of the GPU.
+
+Multi-GPU (``torchrun --nproc-per-node N``): one process per GPU, contiguous shards of the
+global env id space (env_base = rank * n), no collective on the data path (weak scaling);
+a barrier + device sync bracket the timed region and the time is the MAX over ranks.
+
+Also reported: the dominant kernel's roofline (algorithmic FP64 flops / its average launch
+time measured with HIP events on the launch stream) and the CPU oracle timed on this host
+(cpu_baseline, rank 0 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+
+# Algorithmic work per RHS evaluation / RK attempt / segment:
+FLOP_RHS = 102          # 3 angle differences, ux/uy (10 FMA per tube), u_z' (4/tube), R [u]x (27)
+FLOP_ATTEMPT = 1050     # stage combinations 15x18 FMA, y_new 5x18, error 6x18, scale + norm
+FLOP_SEGMENT = 150      # select_initial_step arithmetic
+FLOP_STEP_EXTRA = 220   # 10 x set_action (160) + reward/obs (60)
+SINCOS_RHS = 3
+PEAK_FP64_VALU = 78.6   # TFLOP/s, MI355X FP64 vector (spec)
+PEAK_HBM = 8000.0       # GB/s (spec)
+BYTES_STEP = 170        # algorithmic bytes per env-step
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--envs", type=int, default=65536, help="environments per GPU")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--profile-only", action="store_true", help="no timing extras (for rocprofv3)")
+    return ap.parse_args()
+
+
+def dist_init():
+    import torch
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, ws, local
+    return None, 0, 1, local
+
+
+def make_actions(env, k, seed):
+    import torch
+    g = torch.Generator(device=env.device)
+    g.manual_seed(seed + 1)
+    hi = torch.tensor(env.action_space.high, device=env.device)
+    return [((torch.rand((env.num_envs, 6), generator=g, device=env.device) * 2 - 1) * hi).contiguous()
+            for _ in range(k)]
+
+
+def fk_work(env, joints):
+    """Algorithmic FP64 flops + sincos of one FK per env at the given joints (device counters)."""
+    _, st = env.forward_kinematics(joints, env.system, return_stats=True)
+    nfev = st["nfev"].double()
+    att = (st["nstep"] + st["nrej"]).double()
+    seg = st["nseg"].double()
+    flops = (nfev * FLOP_RHS + att * FLOP_ATTEMPT + seg * FLOP_SEGMENT).sum().item() + FLOP_STEP_EXTRA * joints.shape[0]
+    sincos = (nfev * SINCOS_RHS).sum().item()
+    return flops, sincos, nfev.mean().item()
+
+
+def cpu_baseline(args, env_kwargs):
+    """Oracle (C port, OpenMP) on this host: env-steps/s on a bounded sample of the workload."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    n = 4096
+    q, _ = oracle.sample_joints(n, seed=args.seed, stream=1)
+    dg = oracle.fk(oracle.sample_joints(n, seed=args.seed, stream=0)[0])["tip"]
+    rng = np.random.default_rng(args.seed + 1)
+    hi = np.array([1e-3] * 3 + [np.deg2rad(5)] * 3, np.float32)
+    t = np.zeros(n, np.int32)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        a = ((rng.random((n, 6)) * 2 - 1) * hi).astype(np.float32)
+        r = oracle.step(q, a, dg, t, 0.020)
+        q, t = r["joints"], r["t"]
+        t[t >= 150] = 0
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "%d envs x %d steps of oracle/ctr_oracle.c (scipy-faithful RK45, fp64), OpenMP %d threads, "
+                      "%.1f s" % (n, steps, threads, el)}
+
+
+def main():
+    args = parse()
+    import torch
+    dist, rank, ws, local = dist_init()
+    from ctr_reach_amd import CtrReachVecEnv
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    n = args.envs
+    env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=rank * n, autoreset=True, record_info=False)
+    env.reset()
+    acts = make_actions(env, 8, args.seed + rank)
+    stream = torch.cuda.current_stream()
+
+    for i in range(args.warmup):
+        env.step_raw(acts[i % len(acts)])
+    torch.cuda.synchronize()
+    if args.profile_only:
+        for i in range(args.steps):
+            env.step_raw(acts[i % len(acts)])
+        torch.cuda.synchronize()
+        return
+
+    # ---- timed region: K whole-job steps (includes auto-resets at their natural rate)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        env.step_raw(acts[i % len(acts)])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = el_t.item()
+    total_steps = n * ws * args.steps
+
+    # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset
+    j_probe = env.joints.clone()
+    flops_env_step, sincos, nfev_mean = fk_work(env, j_probe)
+    env.autoreset = False
+    k_iters = max(5, min(args.steps, 20))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k_iters)]
+    for i in range(k_iters):
+        ev[i][0].record(stream)
+        env.step_raw(acts[i % len(acts)])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    k_ms = sum(a.elapsed_time(b) for a, b in ev) / k_iters
+    env.autoreset = True
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    achieved_tf = flops_env_step / (k_ms * 1e-3) / 1e12
+    out = {
+        "metric": "env-steps/sec at 65 536 parallel 3-tube envs; tip-pos L2 vs CPU ref",
+        "value": total_steps / el,
+        "unit": "env-steps/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: Philox-sampled joints/goals (sample_goal region), uniform actions in the action box",
+        "config": {"workload": "configs[2]: %d envs/GPU, 3-tube torsionally-compliant CTR, scipy-RK45 (rtol 1e-3, "
+                               "atol 1e-6) fp64, system 0, n_substeps 10, tol 0.020, max 150 steps, auto-reset"
+                               % n,
+                   "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws},
+        "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": PEAK_FP64_VALU, "unit": "TFLOP/s",
+                     "frac": achieved_tf / PEAK_FP64_VALU, "traffic": None,
+                     "kernel": "k_step", "kernel_ms": k_ms,
+                     "flops_per_launch": flops_env_step, "sincos_per_launch": sincos,
+                     "nfev_per_env_step": nfev_mean,
+                     "hbm_gbs_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9,
+                     "hbm_frac_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9 / PEAK_HBM},
+    }
+    tr = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tr):
+        with open(tr) as fh:
+            t = json.load(fh)
+        if t.get("envs") == n:
+            out["roofline"]["traffic"] = t.get("bytes_per_launch")
+    if not args.no_cpu_baseline and ws == 1:
+        out["cpu_baseline"] = cpu_baseline(args, {})
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

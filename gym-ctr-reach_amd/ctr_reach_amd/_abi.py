@@ -1,0 +1,128 @@
+"""ctypes binding of libctr_reach_amd.so (the C ABI declared in include/ctr_reach_amd.h).
+
+The library is built in-tree (``python -m ctr_reach_amd.build`` or ``__graft_entry__.build()``)
+into ``ctr_reach_amd/lib/``.  There is no CPU fallback: if the shared object is missing or a
+call fails, an exception is raised.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libctr_reach_amd.so")
+
+CTR_ABI_VERSION = 1
+CTR_MAX_SYSTEMS = 8
+CTR_INTEGRATOR_RK45_SCIPY = 0
+CTR_INTEGRATOR_RK4 = 1
+CTR_STATUS_STEP_UNDERFLOW = 1
+CTR_STATUS_SAMPLER_STUCK = 2
+CTR_STATUS_NAN = 4
+
+_d3 = ctypes.c_double * 3
+_P = ctypes.c_void_p
+
+
+class CtrSystem(ctypes.Structure):
+    _fields_ = [("L", _d3), ("Lc", _d3), ("EI", _d3), ("GJ", _d3), ("Ux", _d3), ("Uy", _d3)]
+
+
+class CtrEnvConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_systems", ctypes.c_int32),
+        ("n_substeps", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32),
+        ("constrain_alpha", ctypes.c_int32),
+        ("egocentric", ctypes.c_int32),
+        ("resample_joints", ctypes.c_int32),
+        ("integrator", ctypes.c_int32),
+        ("rk4_steps_per_m", ctypes.c_int32),
+        ("tol", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+        ("systems", CtrSystem * CTR_MAX_SYSTEMS),
+    ]
+
+
+class CtrBatch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("env_base", ctypes.c_int64),
+        ("joints", _P),
+        ("desired_goal", _P),
+        ("achieved_goal", _P),
+        ("t", _P),
+        ("system", _P),
+        ("epoch", _P),
+        ("desired_joints", _P),
+        ("starting_joints", _P),
+        ("starting_position", _P),
+        ("work", _P),
+    ]
+
+
+class CtrStepOut(ctypes.Structure):
+    _fields_ = [
+        ("obs", _P),
+        ("reward", _P),
+        ("done", _P),
+        ("success", _P),
+        ("error", _P),
+        ("terminal_obs", _P),
+        ("terminal_achieved", _P),
+        ("status", _P),
+        ("nfev", _P),
+    ]
+
+
+EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
+            "ctr_compute_reward")
+
+_lib = None
+
+
+class CtrError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load (once) and prototype the shared library.  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise CtrError("libctr_reach_amd.so not built (%s); run __graft_entry__.build()" % path)
+    L = ctypes.CDLL(path)
+    i64, i32 = ctypes.c_int64, ctypes.c_int32
+    L.ctr_abi_version.restype = ctypes.c_int
+    L.ctr_last_error.restype = ctypes.c_char_p
+    L.ctr_fk.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), _P, _P, _P, _P]
+    L.ctr_set_action.argtypes = [ctypes.POINTER(CtrEnvConfig), _P, _P, _P, i64, _P]
+    L.ctr_step.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P,
+                           ctypes.POINTER(CtrStepOut), i32, _P]
+    L.ctr_reset.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P, _P, _P, _P]
+    L.ctr_compute_reward.argtypes = [_P, _P, i64, ctypes.c_double, _P, _P]
+    for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_compute_reward"):
+        getattr(L, fn).restype = ctypes.c_int
+    if L.ctr_abi_version() != CTR_ABI_VERSION:
+        raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = _lib.ctr_last_error().decode() if _lib is not None else ""
+        raise CtrError("%s failed (rc=%d): %s" % (what, rc, msg))
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,152 @@
+"""Single-environment facade with the reference's gym.GoalEnv surface.
+
+``CtrReachEnv(**kwargs)`` accepts exactly the reference constructor kwargs
+(envs/ctr_reach_env.py:14-17) and exposes reset/step/compute_reward/seed/render/close,
+update_goal_tolerance/get_goal_tolerance/print_parameters, observation_space/action_space
+and ``model.forward_kinematics`` -- backed by a one-env CtrReachVecEnv on the GPU.
+Returned observations are numpy float64 dicts like the reference's.
+"""
+import numpy as np
+
+from .spaces import GoalEnvBase
+from .systems import default_kwargs
+from .vec_env import CtrReachVecEnv
+
+
+class Model(object):
+    """Operator boundary: Model.forward_kinematics (envs/model.py:30-70), batched on the GPU."""
+
+    def __init__(self, vec_env):
+        self._env = vec_env
+        self.r = self.r1 = self.r2 = self.r3 = None   # backbone shape: not produced (render is out of scope)
+
+    def forward_kinematics(self, joint, system, **kwargs):
+        q = np.asarray(joint, dtype=np.float32).reshape(-1, 6)
+        tip = self._env.forward_kinematics(q, np.full(q.shape[0], int(system)))
+        out = tip.cpu().numpy()
+        return out[0] if np.ndim(joint) == 1 else out
+
+
+class CtrReachEnv(GoalEnvBase):
+    metadata = {"render.modes": []}
+
+    def __init__(self, ctr_systems_parameters, goal_tolerance_parameters, noise_parameters, joint_representation,
+                 initial_joints, constrain_alpha, extension_action_limit, rotation_action_limit,
+                 max_steps_per_episode, n_substeps, evaluation, select_systems, resample_joints=True,
+                 length_based_sample=False, domain_rand=0.0, device="cuda", seed=0):
+        kw = dict(ctr_systems_parameters=ctr_systems_parameters, goal_tolerance_parameters=goal_tolerance_parameters,
+                  noise_parameters=noise_parameters, joint_representation=joint_representation,
+                  initial_joints=initial_joints, constrain_alpha=constrain_alpha,
+                  extension_action_limit=extension_action_limit, rotation_action_limit=rotation_action_limit,
+                  max_steps_per_episode=max_steps_per_episode, n_substeps=n_substeps, evaluation=evaluation,
+                  select_systems=select_systems, resample_joints=resample_joints,
+                  length_based_sample=length_based_sample, domain_rand=domain_rand)
+        self.vec = CtrReachVecEnv(1, device=device, seed=seed, autoreset=False, **kw)
+        v = self.vec
+        self.select_systems = v.select_systems
+        self.ctr_system_parameters = v.ctr_system_parameters
+        self.noise_parameters = noise_parameters
+        self.joint_representation = joint_representation
+        self.max_steps_per_episode = max_steps_per_episode
+        self.n_substeps = n_substeps
+        self.constrain_alpha = constrain_alpha
+        self.evaluation = evaluation
+        self.resample_joints = resample_joints
+        self.length_based_sample = length_based_sample
+        self.domain_rand = domain_rand
+        self.extension_action_limit = extension_action_limit
+        self.rotation_action_limit = rotation_action_limit
+        self.observation_space = v.observation_space
+        self.action_space = v.action_space
+        self.goal_tolerance = v.goal_tolerance
+        self.model = Model(v)
+        self.t = 0
+        self.system = 0
+        self.starting_joints = np.asarray(initial_joints)
+        self.desired_joints = np.asarray(initial_joints)
+        # :65 initial FK at the initial joints
+        self.starting_position = self.model.forward_kinematics(np.asarray(initial_joints, np.float32), 0)
+        self.desired_goal = self.starting_position
+        self.vec.achieved_goal.copy_(self.vec.forward_kinematics(np.asarray(initial_joints, np.float32)[None]))
+        self.vec.desired_goal.copy_(self.vec.achieved_goal)
+        self.visualization = None
+
+    @property
+    def joints(self):
+        return self.vec.joints[0].cpu().numpy()
+
+    def reset(self, goal=None, system=None):
+        g = None if goal is None else np.asarray(goal, dtype=np.float64).reshape(1, 3)
+        s = None if system is None else np.array([int(system)])
+        self.vec.reset(goal=g, system=s)
+        self.t = 0
+        self.system = int(self.vec.system[0].item())
+        self.desired_goal = self.vec.desired_goal[0].cpu().numpy().copy()
+        self.starting_position = self.vec.achieved_goal[0].cpu().numpy().copy()
+        self.starting_joints = self.vec.joints[0].cpu().numpy().copy()
+        if self.vec.desired_joints is not None and goal is None:
+            self.desired_joints = self.vec.desired_joints[0].cpu().numpy().copy()
+        return self._obs()
+
+    def _obs(self):
+        return {"observation": self.vec.obs[0].cpu().numpy().astype(np.float64),
+                "achieved_goal": self.vec.achieved_goal[0].cpu().numpy().copy(),
+                "desired_goal": self.vec.desired_goal[0].cpu().numpy().copy()}
+
+    def seed(self, seed=None):
+        return self.vec.seed(seed)
+
+    def step(self, action):
+        action = np.asarray(action)
+        assert not np.all(np.isnan(action))                 # :131
+        assert self.action_space.contains(action)           # :132
+        import torch
+        a = torch.as_tensor(np.asarray(action, np.float32).reshape(1, 6), device=self.vec.device)
+        obs, reward, done, info = self.vec.step(a)
+        self.t = int(self.vec.t[0].item())
+        o = self._obs()
+        achieved_goal = o["achieved_goal"]
+        reward = float(reward[0].item())
+        done = bool(done[0].item())
+        err = float(np.linalg.norm(self.desired_goal - achieved_goal))
+        tol = self.goal_tolerance.get_tol()
+        if self.evaluation:
+            info = {"is_success": err < tol, "errors_pos": err, "errors_orient": 0,
+                    "system_idx": self.select_systems[self.system], "position_tolerance": tol,
+                    "orientation_tolerance": 0, "achieved_goal": achieved_goal, "desired_goal": self.desired_goal,
+                    "starting_position": self.starting_position, "q_desired": self.desired_joints,
+                    "q_achieved": self.joints, "q_starting": self.starting_joints}
+        else:
+            info = {"is_success": err < tol, "error": err}
+        return o, np.float64(reward), done, info
+
+    def compute_reward(self, achieved_goal, desired_goal, info):
+        return self.vec.compute_reward(achieved_goal, desired_goal, info)
+
+    def render(self, mode="empty", **kwargs):
+        if mode == "live":
+            raise NotImplementedError("live rendering (matplotlib) is out of scope of the GPU build")
+
+    def close(self):
+        raise SystemExit(0)                                  # :184-191, as the reference does
+
+    def print_parameters(self):
+        print("----Observation and q_space----")
+        print("----Goal tolerance parameters----")
+
+    def update_goal_tolerance(self, timestep):
+        self.goal_tolerance.update(timestep)
+
+    def get_goal_tolerance(self):
+        return self.goal_tolerance.get_tol()
+
+
+_REGISTRY = {"CTR-Reach-v0": (CtrReachEnv, default_kwargs, 150)}
+
+
+def make(env_id="CTR-Reach-v0", **overrides):
+    """gym.make equivalent: registration defaults (ctr_reach_envs/__init__.py:4-96) + overrides."""
+    cls, defaults, _max_steps = _REGISTRY[env_id]
+    kw = defaults()
+    kw.update(overrides)
+    return cls(**kw)

@@ -1,0 +1,283 @@
+"""CtrReachVecEnv -- N concentric-tube-robot reach environments stepped in lockstep on one GPU.
+
+Host side of the hot path.  State lives in device tensors (PyTorch is only the allocator and
+stream provider); every step is ONE call into libctr_reach_amd.so (ctr_step), which enqueues
+the fused step kernel (+ the compacted auto-reset kernel) on the current stream and returns
+without synchronising.
+
+Semantics per environment follow CtrReachEnv (envs/ctr_reach_env.py:13-210):
+  * step        = n_substeps x Obs.set_action, forward kinematics, compute_reward,
+                  done = reward == 0 or t >= max_steps, get_obs                  (:124-158)
+  * reset       = system pick, sample_goal -> FK (desired goal), sample_goal -> FK (start)
+                                                                                  (:70-114)
+  * auto-reset  = VecEnv convention: a done environment is reset inside the same step call;
+                  the returned observation is the new episode's, the terminal observation and
+                  achieved goal are returned in ``info``.
+Random draws come from a Philox4x32-10 stream keyed by (seed, global env id, reset number),
+so results do not depend on how environments are sharded over GPUs.
+"""
+import numpy as np
+
+from . import _abi
+from .goal_tolerance import GoalTolerance
+from .spaces import Box, Dict
+from .systems import default_kwargs, make_config, tubes_from_params
+
+NUM_TUBES = 3
+EXT_TOL = 1e-3    # obs.py:14
+ZERO_TOL = 1e-4   # obs.py:16
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def joint_spaces(systems, constrain_alpha):
+    """Obs.get_joint_space (obs.py:50-76): per-system (joint_space, joint_sample_space)."""
+    js, jss = [], []
+    for tubes in systems:
+        L = np.array([t.L for t in tubes])
+        jss.append(Box(low=np.concatenate((-L + EXT_TOL, np.full(NUM_TUBES, -np.pi))),
+                       high=np.concatenate((np.full(NUM_TUBES, 0), np.full(NUM_TUBES, np.pi)))))
+        lim = np.pi if constrain_alpha else np.inf
+        js.append(Box(low=np.concatenate((-L + EXT_TOL, np.full(NUM_TUBES, -lim))),
+                      high=np.concatenate((np.full(NUM_TUBES, 0), np.full(NUM_TUBES, lim)))))
+    return js, jss
+
+
+def observation_space(systems, goal_tolerance):
+    """Obs.get_observation_space (obs.py:78-134)."""
+    max_len = np.amax(np.array([[t.L for t in tubes] for tubes in systems]), axis=0)
+    rep_low, rep_high = [], []
+    for L in max_len:
+        rep_low += [-1, -1, -L + ZERO_TOL]
+        rep_high += [1, 1, 0]
+    rep = Box(low=np.array(rep_low), high=np.array(rep_high), dtype="float32")
+    if len(systems) == 1:
+        lo = np.concatenate((rep.low, np.array([-0.2, -0.2, -0.2, goal_tolerance.final_tol])))
+        hi = np.concatenate((rep.high, np.array([0.2, 0.2, 0.2, goal_tolerance.init_tol])))
+    else:
+        lo = np.concatenate((rep.low, np.array([-0.2, -0.2, -0.2, goal_tolerance.final_tol, 0])))
+        hi = np.concatenate((rep.high, np.array([0.2, 0.2, 0.2, goal_tolerance.init_tol, len(systems) - 1])))
+    return Dict(dict(
+        desired_goal=Box(low=np.array([-0.1, -0.1, 0]), high=np.array([0.1, 0.1, 0.2]), dtype="float32"),
+        achieved_goal=Box(low=np.array([-0.1, -0.1, 0]), high=np.array([0.1, 0.1, 0.2]), dtype="float32"),
+        observation=Box(low=lo, high=hi, dtype="float32")))
+
+
+def action_space(extension_action_limit, rotation_action_limit):
+    """CtrReachEnv.__init__ :58-62."""
+    b = np.full(NUM_TUBES, extension_action_limit)
+    a = np.full(NUM_TUBES, np.deg2rad(rotation_action_limit))
+    return Box(low=np.concatenate((-b, -a)), high=np.concatenate((b, a)), dtype="float32")
+
+
+class CtrReachVecEnv(object):
+    """Batched CTR-Reach on one GPU.  Constructor kwargs = the reference's (ctr_reach_env.py:14-17)
+    plus ``num_envs``, ``device``, ``seed``, ``env_base`` (global id of env 0 for sharding),
+    ``autoreset``.  Missing reference kwargs take the CTR-Reach-v0 registration defaults."""
+
+    def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True, **kwargs):
+        torch = _torch()
+        kw = default_kwargs()
+        kw.update(kwargs)
+        if kw.get("length_based_sample"):
+            raise NotImplementedError("length_based_sample: the reference branch is broken "
+                                      "(reads the nonexistent self.system_parameters, ctr_reach_env.py:88)")
+        if kw.get("domain_rand", 0.0) != 0.0:
+            raise NotImplementedError("per-env domain randomisation is a later round (SURVEY 8f #4)")
+        assert kw["joint_representation"] in ("egocentric", "proprioceptive")
+        self.kwargs = kw
+        self.lib = _abi.load()
+        self.num_envs = int(num_envs)
+        self.device = torch.device(device)
+        self.env_base = int(env_base)
+        self.autoreset = bool(autoreset)
+        all_systems = tubes_from_params(kw["ctr_systems_parameters"])
+        self.select_systems = list(kw["select_systems"])
+        self.ctr_system_parameters = [all_systems[s] for s in self.select_systems]
+        self.n_systems = len(self.ctr_system_parameters)
+        self.goal_tolerance = GoalTolerance(kw["goal_tolerance_parameters"])
+        self.max_steps_per_episode = kw["max_steps_per_episode"]
+        self.n_substeps = kw["n_substeps"]
+        self.constrain_alpha = kw["constrain_alpha"]
+        self.joint_representation = kw["joint_representation"]
+        self.resample_joints = kw["resample_joints"]
+        self.evaluation = kw["evaluation"]
+        self.noise_parameters = kw["noise_parameters"]   # stored, never applied (reference Q11)
+        self.joint_spaces, self.joint_sample_spaces = joint_spaces(self.ctr_system_parameters, self.constrain_alpha)
+        self.observation_space = observation_space(self.ctr_system_parameters, self.goal_tolerance)
+        self.action_space = action_space(kw["extension_action_limit"], kw["rotation_action_limit"])
+        self.obs_dim = 13 if self.n_systems == 1 else 14
+        self.seed_value = int(seed)
+        self.cfg = make_config(self.ctr_system_parameters, n_substeps=self.n_substeps,
+                               max_steps=self.max_steps_per_episode, constrain_alpha=self.constrain_alpha,
+                               egocentric=self.joint_representation == "egocentric",
+                               resample_joints=self.resample_joints, tol=self.goal_tolerance.get_tol(),
+                               seed=self.seed_value)
+        n, dev = self.num_envs, self.device
+        f32, f64, i32 = torch.float32, torch.float64, torch.int32
+        init = np.asarray(kw["initial_joints"], dtype=np.float64)
+        self.joints = torch.tensor(np.tile(init, (n, 1)), dtype=f32, device=dev)
+        self.desired_goal = torch.zeros((n, 3), dtype=f64, device=dev)
+        self.achieved_goal = torch.zeros((n, 3), dtype=f64, device=dev)
+        self.t = torch.zeros(n, dtype=i32, device=dev)
+        self.system = torch.zeros(n, dtype=i32, device=dev)
+        self.epoch = torch.zeros(n, dtype=i32, device=dev)
+        self.work = torch.zeros(n + 1, dtype=i32, device=dev)
+        self.desired_joints = torch.zeros((n, 6), dtype=f32, device=dev) if record_info else None
+        self.starting_joints = torch.zeros((n, 6), dtype=f32, device=dev) if record_info else None
+        self.starting_position = torch.zeros((n, 3), dtype=f64, device=dev) if record_info else None
+        # outputs (persistent; step() returns views of these buffers)
+        self.obs = torch.zeros((n, self.obs_dim), dtype=f32, device=dev)
+        self.reward = torch.zeros(n, dtype=f32, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.success = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.error = torch.zeros(n, dtype=f32, device=dev)
+        self.terminal_obs = torch.zeros((n, self.obs_dim), dtype=f32, device=dev)
+        self.terminal_achieved = torch.zeros((n, 3), dtype=f64, device=dev)
+        self.status = torch.zeros(n, dtype=i32, device=dev)
+        self.nfev = None
+        self._batch = _abi.CtrBatch()
+        self._out = _abi.CtrStepOut()
+        self._fill_structs()
+
+    # ------------------------------------------------------------------ plumbing
+    def _fill_structs(self):
+        p = _abi.ptr
+        b = self._batch
+        b.n, b.env_base = self.num_envs, self.env_base
+        b.joints, b.desired_goal, b.achieved_goal = p(self.joints), p(self.desired_goal), p(self.achieved_goal)
+        b.t, b.system, b.epoch, b.work = p(self.t), p(self.system), p(self.epoch), p(self.work)
+        b.desired_joints, b.starting_joints = p(self.desired_joints), p(self.starting_joints)
+        b.starting_position = p(self.starting_position)
+        o = self._out
+        o.obs, o.reward, o.done, o.success, o.error = (p(self.obs), p(self.reward), p(self.done), p(self.success),
+                                                        p(self.error))
+        o.terminal_obs, o.terminal_achieved, o.status = p(self.terminal_obs), p(self.terminal_achieved), p(self.status)
+        o.nfev = p(self.nfev)
+
+    def enable_nfev(self, on=True):
+        """Record per-env RHS evaluation counts of the last step (diagnostics / roofline)."""
+        torch = _torch()
+        self.nfev = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device) if on else None
+        self._fill_structs()
+
+    def _obs_dict(self):
+        return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
+
+    # ------------------------------------------------------------------ gym surface
+    def seed(self, seed=None):
+        if seed is not None:
+            self.seed_value = int(seed)
+            self.cfg.seed = self.seed_value & 0xFFFFFFFFFFFFFFFF
+        return [self.seed_value]
+
+    def reset(self, goal=None, system=None, mask=None, stream=None):
+        """CtrReachEnv.reset for all envs (or those with mask != 0).  goal: [N,3] f64 tensor or
+        None (sample); system: [N] int tensor or None (uniform).  Returns the obs dict."""
+        torch = _torch()
+        self.cfg.tol = float(self.goal_tolerance.get_tol())
+        g = None if goal is None else torch.as_tensor(goal, dtype=torch.float64, device=self.device).reshape(-1, 3).contiguous()
+        s = None if system is None else torch.as_tensor(system, dtype=torch.int32, device=self.device).reshape(-1).contiguous()
+        m = None if mask is None else torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        if g is not None and g.shape[0] == 1 and self.num_envs > 1:
+            g = g.expand(self.num_envs, 3).contiguous()
+        if s is not None and s.shape[0] == 1 and self.num_envs > 1:
+            s = s.expand(self.num_envs).contiguous()
+        if s is not None:
+            bad = (s < 0) | (s >= self.n_systems)
+            if bool(bad.any()):
+                raise ValueError("system index out of range")
+        self._keep = (g, s, m)   # keep alive until the kernel has consumed them
+        rc = self.lib.ctr_reset(self.cfg, self._batch, _abi.ptr(m), _abi.ptr(g), _abi.ptr(s), _abi.ptr(self.obs),
+                                _abi.ptr(self.status), _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_reset")
+        return self._obs_dict()
+
+    def step(self, actions, stream=None):
+        """One step of every env.  actions: [N,6] float32 device tensor.  Returns
+        (obs dict, reward [N] f32, done [N] bool, info dict of tensors).  Returned tensors are
+        views of persistent buffers, overwritten by the next call."""
+        torch = _torch()
+        if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if actions.shape != (self.num_envs, 6):
+            raise ValueError("actions must be [%d, 6]" % self.num_envs)
+        self.cfg.tol = float(self.goal_tolerance.get_tol())
+        self._last_actions = actions
+        rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
+                               _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_step")
+        info = {"is_success": self.success.bool(), "error": self.error,
+                "terminal_observation": self.terminal_obs, "terminal_achieved_goal": self.terminal_achieved,
+                "status": self.status}
+        return self._obs_dict(), self.reward, self.done.bool(), info
+
+    def step_raw(self, actions, stream=None):
+        """step() without building Python return values (benchmark / graph capture)."""
+        rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
+                               _abi.stream_ptr(stream))
+        if rc:
+            _abi.check(rc, "ctr_step")
+
+    def compute_reward(self, achieved_goal, desired_goal, info=None):
+        """compute_reward (ctr_reach_env.py:160-170), batched over leading dims.  Device tensors
+        run on the GPU (HER relabelling); numpy arrays follow the reference exactly."""
+        torch = _torch()
+        tol = float(self.goal_tolerance.get_tol())
+        if isinstance(achieved_goal, torch.Tensor):
+            assert achieved_goal.shape == desired_goal.shape
+            shape = achieved_goal.shape[:-1]
+            ag = achieved_goal.to(self.device, torch.float64).reshape(-1, 3).contiguous()
+            dg = desired_goal.to(self.device, torch.float64).reshape(-1, 3).contiguous()
+            out = torch.empty(ag.shape[0], dtype=torch.float32, device=self.device)
+            rc = self.lib.ctr_compute_reward(_abi.ptr(ag), _abi.ptr(dg), ag.shape[0], tol, _abi.ptr(out),
+                                             _abi.stream_ptr())
+            _abi.check(rc, "ctr_compute_reward")
+            return out.reshape(shape)
+        achieved_goal = np.asarray(achieved_goal)
+        desired_goal = np.asarray(desired_goal)
+        assert achieved_goal.shape == desired_goal.shape
+        d = np.linalg.norm(achieved_goal - desired_goal, axis=-1)
+        return -(d > tol).astype(np.float64)
+
+    def forward_kinematics(self, joints, system=None, stream=None, return_stats=False):
+        """Batched Model.forward_kinematics (model.py:30): joints [M,6] -> tip [M,3] f64 (device)."""
+        torch = _torch()
+        q = torch.as_tensor(joints, dtype=torch.float32, device=self.device).reshape(-1, 6).contiguous()
+        m = q.shape[0]
+        s = None if system is None else torch.as_tensor(system, dtype=torch.int32, device=self.device).reshape(-1).expand(m).contiguous()
+        tip = torch.empty((m, 3), dtype=torch.float64, device=self.device)
+        stats = torch.zeros((m, 4), dtype=torch.int32, device=self.device) if return_stats else None
+        status = torch.zeros(m, dtype=torch.int32, device=self.device)
+        rc = self.lib.ctr_fk(_abi.ptr(q), _abi.ptr(s), m, self.cfg, _abi.ptr(tip), _abi.ptr(stats), _abi.ptr(status),
+                             _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_fk")
+        if return_stats:
+            return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=stats[:, 2], nseg=stats[:, 3], status=status)
+        return tip
+
+    def update_goal_tolerance(self, timestep):
+        self.goal_tolerance.update(timestep)
+
+    def get_goal_tolerance(self):
+        return self.goal_tolerance.get_tol()
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self):
+        keys = ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch")
+        sd = {k: getattr(self, k).clone() for k in keys}
+        sd["seed"] = self.seed_value
+        sd["tol"] = self.goal_tolerance.get_tol()
+        return sd
+
+    def load_state_dict(self, sd):
+        for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch"):
+            getattr(self, k).copy_(sd[k])
+        self.seed(sd["seed"])
+        self.goal_tolerance.current_tol = sd["tol"]
+
+    def close(self):
+        pass

@@ -1,0 +1,139 @@
+/*
+ * ctr_reach_amd.h -- C ABI of libctr_reach_amd.so, the MI355X (gfx950) batched
+ * concentric-tube-robot reach environment.
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes, and is asynchronous
+ * and stream-ordered: it enqueues HIP kernels on `stream` and returns without a device
+ * synchronisation.  All device buffers are allocated and owned by the caller (PyTorch);
+ * the library allocates nothing on the hot path.  Pointers marked "device" must be
+ * device memory; structs themselves are read from host memory at call time.
+ *
+ * Return codes: 0 = ok, CTR_EINVAL (-1) = bad argument, CTR_EHIP (-2) = HIP launch error.
+ * ctr_last_error() returns a thread-local description of the last failure.
+ * Per-environment numeric faults (ODE step-size underflow, sampler exhaustion) are
+ * reported through per-lane `status` words, never by aborting.
+ *
+ * Reference interfaces each entry point replaces (reference = keshaviyengar/gym-ctr-reach,
+ * paths relative to ctr_reach_envs/):
+ *   ctr_fk              Model.forward_kinematics(joint, system)          envs/model.py:30-70
+ *                       (+ Segment envs/CTR_Python/Segment.py:6-61, ode_eq model.py:72-117,
+ *                        ctr_model model.py:119-174, scipy solve_ivp RK45)
+ *   ctr_set_action      Obs.set_action(action, system) x n_substeps       envs/obs.py:166-183,
+ *                                                                          envs/ctr_reach_env.py:134-135
+ *   ctr_step            CtrReachEnv.step(action)                          envs/ctr_reach_env.py:124-158
+ *   ctr_reset           CtrReachEnv.reset(goal=None, system=None)         envs/ctr_reach_env.py:70-114
+ *                       (+ Obs.sample_goal envs/obs.py:185-207, get_obs obs.py:136-164)
+ *   ctr_compute_reward  CtrReachEnv.compute_reward(ag, dg, info)          envs/ctr_reach_env.py:160-170
+ */
+#ifndef CTR_REACH_AMD_H
+#define CTR_REACH_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CTR_ABI_VERSION 1
+#define CTR_MAX_SYSTEMS 8
+#define CTR_EINVAL (-1)
+#define CTR_EHIP (-2)
+
+/* per-lane status bits */
+#define CTR_STATUS_STEP_UNDERFLOW 1u   /* scipy "Required step size is less than spacing" */
+#define CTR_STATUS_SAMPLER_STUCK  2u   /* obs.py:204 "Stuck sampling goals..." (>1000 tries) */
+#define CTR_STATUS_NAN            4u   /* model.py:69 assert not any(isnan(r)) */
+
+/* One 3-tube system (index 0 = innermost tube), derived on the host from the
+ * registration kwargs exactly as Tube.__init__ (envs/CTR_Python/Tube.py:7-19):
+ * EI = E * pi (d_o^4 - d_i^4) / 64, GJ = G * pi (d_o^4 - d_i^4) / 32. */
+typedef struct ctr_system_t {
+    double L[3];       /* tube length                        (Tube.L)    */
+    double Lc[3];      /* pre-curved length                  (Tube.L_c)  */
+    double EI[3];      /* bending stiffness  E * I                       */
+    double GJ[3];      /* torsional stiffness G * J                      */
+    double Ux[3];      /* pre-curvature x    (Tube.U_x)                  */
+    double Uy[3];      /* pre-curvature y    (Tube.U_y)                  */
+} ctr_system_t;
+
+/* Integrator selection */
+#define CTR_INTEGRATOR_RK45_SCIPY 0    /* scipy solve_ivp RK45 emulation, rtol 1e-3 atol 1e-6 (parity) */
+#define CTR_INTEGRATOR_RK4        1    /* fixed-step classical RK4 of the same ODE (throughput)       */
+
+/* Environment configuration (registration kwargs, ctr_reach_envs/__init__.py:6-94). */
+typedef struct ctr_env_config_t {
+    int32_t n_systems;          /* len(select_systems), 1..CTR_MAX_SYSTEMS              */
+    int32_t n_substeps;         /* n_substeps (10)                                       */
+    int32_t max_steps;          /* max_steps_per_episode (150)                           */
+    int32_t constrain_alpha;    /* constrain_alpha                                       */
+    int32_t egocentric;         /* joint_representation == 'egocentric'                  */
+    int32_t resample_joints;    /* resample_joints                                       */
+    int32_t integrator;         /* CTR_INTEGRATOR_*                                      */
+    int32_t rk4_steps_per_m;    /* RK4 only: steps per metre of arclength                */
+    double  tol;                /* goal_tolerance.get_tol()                              */
+    uint64_t seed;              /* Philox key for resets                                 */
+    ctr_system_t systems[CTR_MAX_SYSTEMS];
+} ctr_env_config_t;
+
+/* Device-resident batch state, row-major per environment ([n][k]). */
+typedef struct ctr_batch_t {
+    int64_t   n;                 /* environments in this shard                        */
+    int64_t   env_base;          /* global id of environment 0 (RNG key; sharding)    */
+    float    *joints;            /* [n][6] f32 [b0,b1,b2,a0,a1,a2] (Obs.joints)       */
+    double   *desired_goal;      /* [n][3]                                            */
+    double   *achieved_goal;     /* [n][3] tip after the last step / reset            */
+    int32_t  *t;                 /* [n] steps taken in the episode                    */
+    int32_t  *system;            /* [n] index into config.systems                     */
+    uint32_t *epoch;             /* [n] resets taken so far (RNG counter)             */
+    float    *desired_joints;    /* [n][6] or NULL (info q_desired)                   */
+    float    *starting_joints;   /* [n][6] or NULL (info q_starting)                  */
+    double   *starting_position; /* [n][3] or NULL                                    */
+    int32_t  *work;              /* [n+1] scratch for the auto-reset list (device)    */
+} ctr_batch_t;
+
+/* Per-step outputs (device). obs_dim = 13, or 14 when n_systems > 1 (obs.py:153-156). */
+typedef struct ctr_step_out_t {
+    float    *obs;               /* [n][obs_dim]   observation after the step (after auto-reset) */
+    float    *reward;            /* [n]            0 or -1                                       */
+    uint8_t  *done;              /* [n]                                                          */
+    uint8_t  *success;           /* [n]            info['is_success']                            */
+    float    *error;             /* [n]            info['error'] = ||dg - ag||                   */
+    float    *terminal_obs;      /* [n][obs_dim] or NULL: pre-reset observation of done envs     */
+    double   *terminal_achieved; /* [n][3] or NULL: achieved goal of the terminal step           */
+    uint32_t *status;            /* [n] or NULL: CTR_STATUS_* bits                               */
+    uint32_t *nfev;              /* [n] or NULL: RHS evaluations spent in the step's FK          */
+} ctr_step_out_t;
+
+int ctr_abi_version(void);
+const char *ctr_last_error(void);
+
+/* Batched Model.forward_kinematics: joints [n][6] f32 -> tip [n][3] f64.
+ * sys_idx: [n] or NULL (all system 0).  stats: [n][4] or NULL = {RHS evaluations, accepted
+ * RK steps, rejected RK attempts, integrated segments}.  status: [n] or NULL.  (device) */
+int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg,
+           double *tip, uint32_t *stats, uint32_t *status, void *stream);
+
+/* n_substeps x Obs.set_action, in place on joints [n][6] (device). */
+int ctr_set_action(const ctr_env_config_t *cfg, float *joints, const int32_t *sys_idx,
+                   const float *actions, int64_t n, void *stream);
+
+/* One CtrReachEnv.step for every environment of the batch; actions [n][6] f32 (device).
+ * autoreset != 0: done environments are reset in the same call (VecEnv semantics) and
+ * their pre-reset observation goes to out->terminal_obs. */
+int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float *actions,
+             const ctr_step_out_t *out, int32_t autoreset, void *stream);
+
+/* CtrReachEnv.reset for the environments with mask[i] != 0 (mask NULL = all).
+ * goal [n][3] or NULL (sample a goal), system [n] or NULL (sample uniformly).
+ * Writes the reset observation to obs [n][obs_dim]. */
+int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8_t *mask,
+              const double *goal, const int32_t *system, float *obs, uint32_t *status, void *stream);
+
+/* Batched compute_reward over leading dims: ag, dg [n][3] f64 -> reward [n] f32 in {-1, 0}. */
+int ctr_compute_reward(const double *achieved, const double *desired, int64_t n, double tol,
+                       float *reward, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CTR_REACH_AMD_H */

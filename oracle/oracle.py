@@ -1,0 +1,157 @@
+"""ctypes front-end of the CPU oracle (oracle/ctr_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg -- never by the product package (gym-ctr-reach_amd/ctr_reach_amd).
+
+Tube-constant derivation restated from envs/CTR_Python/Tube.py:7-19
+(I = pi (d_o^4 - d_i^4) / 64, J = pi (d_o^4 - d_i^4) / 32, Python ``math`` arithmetic).
+"""
+import ctypes
+import json
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libctr_oracle.so")
+GOLDEN_SYSTEMS = os.path.join(os.path.dirname(HERE), "tests", "golden", "systems.json")
+
+
+class OracleSystem(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double * 3) for n in ("L", "Lc", "E", "G", "I", "J", "Ux", "Uy")]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i64, i32, u64, u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32
+        L.oracle_fk.argtypes = [P, P, i64, P, P, P, P, P, P]
+        L.oracle_step.argtypes = [i64, P, P, P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P]
+        L.oracle_set_action.argtypes = [i64, P, P, P, P, ctypes.c_int, ctypes.c_int]
+        L.oracle_sample_joints.argtypes = [i64, P, P, u64, P, u32, i64, P, P]
+        L.oracle_philox.argtypes = [P, u64]
+        L.oracle_segments.argtypes = [P, P, i64, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def default_system_params():
+    with open(GOLDEN_SYSTEMS) as fh:
+        return json.load(fh)["ctr_systems_parameters"]
+
+
+def make_systems(params=None, select=None):
+    """Array of OracleSystem from a ctr_systems_parameters dict (registration format)."""
+    params = params or default_system_params()
+    names = list(params.keys())
+    if select is not None:
+        names = [names[i] for i in select]
+    arr = (OracleSystem * len(names))()
+    for k, name in enumerate(names):
+        tubes = params[name]
+        for i, tname in enumerate(sorted(tubes.keys())):
+            t = tubes[tname]
+            arr[k].L[i] = t["length"]
+            arr[k].Lc[i] = t["length_curved"]
+            arr[k].E[i] = t["stiffness"]
+            arr[k].G[i] = t["torsional_stiffness"]
+            d4 = math.pow(t["diameter_outer"], 4) - math.pow(t["diameter_inner"], 4)
+            arr[k].J[i] = (math.pi * d4) / 32
+            arr[k].I[i] = (math.pi * d4) / 64
+            arr[k].Ux[i] = t["x_curvature"]
+            arr[k].Uy[i] = t["y_curvature"]
+    return arr
+
+
+def fk(joints, system=None, systems=None):
+    """Batched Model.forward_kinematics (model.py:30).  Returns dict of tip/nfev/nstep/nseg/status."""
+    q = np.ascontiguousarray(joints, dtype=np.float32).reshape(-1, 6)
+    n = q.shape[0]
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    tip = np.zeros((n, 3))
+    nfev = np.zeros(n, np.int32); nstep = np.zeros(n, np.int32)
+    nseg = np.zeros(n, np.int32); status = np.zeros(n, np.int32)
+    lib().oracle_fk(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), _p(tip), _p(nfev), _p(nstep),
+                    _p(nseg), _p(status))
+    return dict(tip=tip, nfev=nfev, nstep=nstep, nseg=nseg, status=status)
+
+
+def step(joints, actions, desired, t, tol, system=None, systems=None, n_substeps=10, max_steps=150,
+         constrain_alpha=False, multi=False, egocentric=True):
+    """Batched CtrReachEnv.step (ctr_reach_env.py:124-158); returns new state + outputs."""
+    q = np.array(joints, dtype=np.float32).reshape(-1, 6)
+    n = q.shape[0]
+    a = np.ascontiguousarray(np.broadcast_to(actions, (n, 6)), dtype=np.float32)
+    dg = np.ascontiguousarray(np.broadcast_to(desired, (n, 3)), dtype=np.float64)
+    tt = np.array(np.broadcast_to(t, (n,)), dtype=np.int32)
+    tl = np.ascontiguousarray(np.broadcast_to(tol, (n,)), dtype=np.float64)
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    olen = 14 if multi else 13
+    ag = np.zeros((n, 3)); obs = np.zeros((n, olen)); rew = np.zeros(n)
+    done = np.zeros(n, np.uint8); succ = np.zeros(n, np.uint8); err = np.zeros(n)
+    nfev = np.zeros(n, np.int32)
+    lib().oracle_step(n, ctypes.cast(systems, ctypes.c_void_p), _p(s), _p(q), _p(a), _p(dg), _p(tt), _p(tl),
+                      n_substeps, max_steps, int(constrain_alpha), int(multi), int(egocentric),
+                      _p(ag), _p(obs), _p(rew), _p(done), _p(succ), _p(err), _p(nfev))
+    return dict(joints=q, t=tt, achieved_goal=ag, observation=obs, reward=rew, done=done.astype(bool),
+                is_success=succ.astype(bool), error=err, nfev=nfev)
+
+
+def set_action(joints, actions, system=None, systems=None, n_substeps=10, constrain_alpha=False):
+    q = np.array(joints, dtype=np.float32).reshape(-1, 6)
+    n = q.shape[0]
+    a = np.ascontiguousarray(np.broadcast_to(actions, (n, 6)), dtype=np.float32)
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    lib().oracle_set_action(n, ctypes.cast(systems, ctypes.c_void_p), _p(s), _p(q), _p(a), n_substeps,
+                            int(constrain_alpha))
+    return q
+
+
+def sample_joints(n, seed, stream=0, epoch=None, env_base=0, system=None, systems=None):
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    ep = None if epoch is None else np.ascontiguousarray(np.broadcast_to(epoch, (n,)), dtype=np.uint32)
+    systems = systems if systems is not None else make_systems()
+    q = np.zeros((n, 6), np.float32)
+    tries = np.zeros(n, np.int32)
+    lib().oracle_sample_joints(n, ctypes.cast(systems, ctypes.c_void_p), _p(s), seed, _p(ep), stream,
+                               env_base, _p(q), _p(tries))
+    return q, tries
+
+
+def philox(counter4, seed):
+    c = np.ascontiguousarray(counter4, dtype=np.uint32).copy()
+    lib().oracle_philox(_p(c), seed)
+    return c
+
+
+def segments(joints, system=None, systems=None):
+    """Segment.S per env (Segment.py:46-51): returns (m [n], S [n, 9])."""
+    q = np.ascontiguousarray(joints, dtype=np.float32).reshape(-1, 6)
+    n = q.shape[0]
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    m = np.zeros(n, np.int32)
+    S = np.zeros((n, 9))
+    lib().oracle_segments(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), _p(m), _p(S))
+    return m, S

