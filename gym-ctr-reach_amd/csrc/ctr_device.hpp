@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "ctr_reach_amd.h"
+#include "ctr_math.hpp"
 
 namespace ctr {
 
@@ -148,19 +149,35 @@ __device__ __forceinline__ SegPar seg_par(const ctr_system_t &sy, uint32_t bits6
 }
 
 // ------------------------------------------------------------------------------------------
-// RHS of the torsionally compliant model (model.py:72-117).  The three distinct relative
-// angles alpha_i - alpha_j are evaluated once each (sin odd, cos even).
+// RHS of the torsionally compliant model (model.py:72-117), split in two parts:
+//   trig_of(alpha)          the three relative-angle sin/cos pairs (the transcendental part;
+//                           depends on the alpha components only)
+//   rhs_core(p, trig, y)    d(u_z)/ds and dR/ds for one segment's constants
+// The remaining derivative components are copies and are never materialised:
+//   d(alpha_j)/ds = u_z,j if tube j is present else 0          (model.py:98)
+//   dr/ds = R e3 = column 3 of R                               (model.py:104-109)
 // ------------------------------------------------------------------------------------------
-template <bool HAS_UY>
-__device__ __forceinline__ void rhs(const SegPar &p, const double *y, double *dy)
+struct Trig {
+    double c10, s10, c20, s20, c21, s21;   // cos/sin(alpha_i - alpha_j)
+};
+
+__device__ __forceinline__ Trig trig_of(const double al[3])
 {
-    double s10, c10, s20, c20, s21, c21;
-    sincos(y[4] - y[3], &s10, &c10);
-    sincos(y[5] - y[3], &s20, &c20);
-    sincos(y[5] - y[4], &s21, &c21);
-    // c[i][j] = cos(a_i - a_j), s[i][j] = sin(a_i - a_j)
-    const double c[3][3] = {{1.0, c10, c20}, {c10, 1.0, c21}, {c20, c21, 1.0}};
-    const double s[3][3] = {{0.0, -s10, -s20}, {s10, 0.0, -s21}, {s20, s21, 0.0}};
+    Trig t;
+    ctr_math::sincos_cw(al[1] - al[0], &t.s10, &t.c10);
+    ctr_math::sincos_cw(al[2] - al[0], &t.s20, &t.c20);
+    // alpha_2 - alpha_1 = (alpha_2 - alpha_0) - (alpha_1 - alpha_0): angle-difference identity
+    t.c21 = t.c20 * t.c10 + t.s20 * t.s10;
+    t.s21 = t.s20 * t.c10 - t.c20 * t.s10;
+    return t;
+}
+
+template <bool HAS_UY>
+__device__ __forceinline__ void rhs_core(const SegPar &p, const Trig &t, const double uz[3], const double R[9],
+                                         double duz[3], double dR[9])
+{
+    const double c[3][3] = {{1.0, t.c10, t.c20}, {t.c10, 1.0, t.c21}, {t.c20, t.c21, 1.0}};
+    const double s[3][3] = {{0.0, -t.s10, -t.s20}, {t.s10, 0.0, -t.s21}, {t.s20, t.s21, 0.0}};
     double ux[3], uy[3];
     #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -179,19 +196,16 @@ __device__ __forceinline__ void rhs(const SegPar &p, const double *y, double *dy
     }
     #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        double tz = HAS_UY ? (ux[j] * p.uy0[j] - uy[j] * p.ux0[j]) : (-uy[j] * p.ux0[j]);
-        dy[j] = p.kz[j] * tz;                                  // model.py:97 (0 if absent)
-        dy[3 + j] = ((p.present >> j) & 1u) ? y[j] : 0.0;      // model.py:98
+        const double tz = HAS_UY ? (ux[j] * p.uy0[j] - uy[j] * p.ux0[j]) : (-uy[j] * p.ux0[j]);
+        duz[j] = p.kz[j] * tz;                                   // model.py:97 (0 if absent)
     }
-    const double *R = y + 9;
-    const double uz = y[0], a = ux[0], b = uy[0];
-    dy[6] = R[2]; dy[7] = R[5]; dy[8] = R[8];                  // dr = R e3
+    const double u0 = uz[0], a = ux[0], b = uy[0];
     #pragma unroll
-    for (int r = 0; r < 3; ++r) {                               // dR = R [u]x
+    for (int r = 0; r < 3; ++r) {                                 // dR = R [u]x  (model.py:103-110)
         const double r0 = R[3 * r], r1 = R[3 * r + 1], r2 = R[3 * r + 2];
-        dy[9 + 3 * r + 0] = r1 * uz - r2 * b;
-        dy[9 + 3 * r + 1] = r2 * a - r0 * uz;
-        dy[9 + 3 * r + 2] = r0 * b - r1 * a;
+        dR[3 * r + 0] = r1 * u0 - r2 * b;
+        dR[3 * r + 1] = r2 * a - r0 * u0;
+        dR[3 * r + 2] = r0 * b - r1 * a;
     }
 }
 
@@ -209,18 +223,26 @@ constexpr double B0 = 35.0 / 384, B2 = 500.0 / 1113, B3 = 125.0 / 192, B4 = -218
 constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 17253.0 / 339200,
                  E5 = -22.0 / 525, E6 = 1.0 / 40;
 constexpr double RTOL = 1e-3, ATOL = 1e-6;
+constexpr double INV_SQRT18 = 0.23570226039551584;
 }  // namespace rk
 
 struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
 
-__device__ __forceinline__ double rms18(const double *x)
+// Stage derivative storage: u_z' (3), alpha' (3), R' (9).  r' = column 3 of the stage input
+// R is folded straight into the B / E accumulators instead of being stored.
+struct Stage {
+    double uz[3], al[3], R[9];
+};
+
+// Full derivative at a state y whose (u_z, R) derivatives are d: builds alpha' and r'.
+__device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const double *uz, const double *R, Stage &k,
+                                         double rcol[3])
 {
-    double s = 0.0;
     #pragma unroll
-    for (int i = 0; i < NS; ++i) s += x[i] * x[i];
-    return sqrt(s) * 0.23570226039551584;   // 1/sqrt(18)
+    for (int j = 0; j < 3; ++j) k.al[j] = ((p.present >> j) & 1u) ? uz[j] : 0.0;
+    rcol[0] = R[2]; rcol[1] = R[5]; rcol[2] = R[8];
 }
 
 // Forward kinematics of one lane: joints (f32, promoted to f64 as model.py:51) -> tip (f64).
@@ -231,18 +253,20 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};
     const Seg sg = seg_build(sy, beta);
 
-    double y[NS];
+    // state y = [u_z(3), alpha(3), r(3), R(9)]
+    double yu[3] = {0.0, 0.0, 0.0};
+    double ya[3] = {(double)q[3], (double)q[4], (double)q[5]};
+    double yr[3] = {0.0, 0.0, 0.0};
+    double yR[9];
     {
-        const double a0 = (double)q[3];
         double s0, c0;
-        sincos(a0, &s0, &c0);
-        #pragma unroll
-        for (int i = 0; i < NS; ++i) y[i] = 0.0;
-        y[3] = (double)q[3]; y[4] = (double)q[4]; y[5] = (double)q[5];
-        y[9] = c0; y[10] = -s0; y[12] = s0; y[13] = c0; y[17] = 1.0;   // R0 = Rz(alpha_0)
+        ctr_math::sincos_cw(ya[0], &s0, &c0);                    // R0 = Rz(alpha_0)  model.py:57-60
+        yR[0] = c0; yR[1] = -s0; yR[2] = 0.0;
+        yR[3] = s0; yR[4] = c0;  yR[5] = 0.0;
+        yR[6] = 0.0; yR[7] = 0.0; yR[8] = 1.0;
     }
-
-    double f[NS];
+    Trig ty = trig_of(ya);          // trig of the current state's alphas (reused at segment starts)
+    Stage f;                        // FSAL derivative at y (alpha' and r' implied by y)
     SegPar p;
     double t = 0.0, tb = 0.0, ha = 0.0, min_step = 0.0, prev_end = 0.0;
     uint32_t remaining = sg.kept;   // kept gaps not yet integrated, in arclength order
@@ -250,41 +274,75 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
 
     for (;;) {
         if (need_init) {
-            // advance to the next kept gap (Segment.S), or finish
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
             p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u));
             const double endk = sel9(sg.end, k);
-            const double a = prev_end, b = endk - 1e-6;     // model.py:141 linspace endpoints
+            const double a = prev_end, b = endk - 1e-6;          // model.py:141 linspace endpoints
             const double t0 = fmin(a, b);
-            tb = fmax(a, b);                                 // :145-151 sorted span
+            tb = fmax(a, b);                                      // :145-151 sorted span
             prev_end = endk;
-            rhs<HAS_UY>(p, y, f);                            // RungeKutta.__init__: f = fun(t0, y0)
+            // RungeKutta.__init__: f = fun(t0, y0) -- the trig of y is already known
+            rhs_core<HAS_UY>(p, ty, yu, yR, f.uz, f.R);
+            double fr[3];
+            stage_at(p, ty, yu, yR, f, fr);
             st.nfev++;
             st.nseg++;
             const double interval = tb - t0;
-            if (interval == 0.0) continue;                   // OdeSolver.step: t == t_bound
+            if (interval == 0.0) continue;                        // OdeSolver.step: t == t_bound
             // select_initial_step (common.py:68-140), order 4, direction +1
-            double sc[NS], tmp[NS];
+            double isc_u[3], isc_a[3], isc_r[3], isc_R[9];
             #pragma unroll
-            for (int i = 0; i < NS; ++i) sc[i] = ATOL + fabs(y[i]) * RTOL;
+            for (int i = 0; i < 3; ++i) {
+                isc_u[i] = 1.0 / (ATOL + fabs(yu[i]) * RTOL);
+                isc_a[i] = 1.0 / (ATOL + fabs(ya[i]) * RTOL);
+                isc_r[i] = 1.0 / (ATOL + fabs(yr[i]) * RTOL);
+            }
             #pragma unroll
-            for (int i = 0; i < NS; ++i) tmp[i] = y[i] / sc[i];
-            const double d0 = rms18(tmp);
+            for (int i = 0; i < 9; ++i) isc_R[i] = 1.0 / (ATOL + fabs(yR[i]) * RTOL);
+            double s0 = 0.0, s1 = 0.0;
             #pragma unroll
-            for (int i = 0; i < NS; ++i) tmp[i] = f[i] / sc[i];
-            const double d1 = rms18(tmp);
+            for (int i = 0; i < 3; ++i) {
+                s0 += (yu[i] * isc_u[i]) * (yu[i] * isc_u[i]) + (ya[i] * isc_a[i]) * (ya[i] * isc_a[i]) +
+                      (yr[i] * isc_r[i]) * (yr[i] * isc_r[i]);
+                s1 += (f.uz[i] * isc_u[i]) * (f.uz[i] * isc_u[i]) + (f.al[i] * isc_a[i]) * (f.al[i] * isc_a[i]) +
+                      (fr[i] * isc_r[i]) * (fr[i] * isc_r[i]);
+            }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                s0 += (yR[i] * isc_R[i]) * (yR[i] * isc_R[i]);
+                s1 += (f.R[i] * isc_R[i]) * (f.R[i] * isc_R[i]);
+            }
+            const double d0 = sqrt(s0) * INV_SQRT18, d1 = sqrt(s1) * INV_SQRT18;
             double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
             h0 = fmin(h0, interval);
-            double y1[NS], f1[NS];
+            double u1[3], a1[3], R1[9];
             #pragma unroll
-            for (int i = 0; i < NS; ++i) y1[i] = y[i] + h0 * f[i];
-            rhs<HAS_UY>(p, y1, f1);
+            for (int i = 0; i < 3; ++i) { u1[i] = yu[i] + h0 * f.uz[i]; a1[i] = ya[i] + h0 * f.al[i]; }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) R1[i] = yR[i] + h0 * f.R[i];
+            Stage f1;
+            double f1r[3];
+            {
+                const Trig t1 = trig_of(a1);
+                rhs_core<HAS_UY>(p, t1, u1, R1, f1.uz, f1.R);
+                stage_at(p, t1, u1, R1, f1, f1r);
+            }
             st.nfev++;
+            double s2 = 0.0;
             #pragma unroll
-            for (int i = 0; i < NS; ++i) tmp[i] = (f1[i] - f[i]) / sc[i];
-            const double d2 = rms18(tmp) / h0;
+            for (int i = 0; i < 3; ++i) {
+                const double du = (f1.uz[i] - f.uz[i]) * isc_u[i], da = (f1.al[i] - f.al[i]) * isc_a[i],
+                             dr = (f1r[i] - fr[i]) * isc_r[i];
+                s2 += du * du + da * da + dr * dr;
+            }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                const double dR = (f1.R[i] - f.R[i]) * isc_R[i];
+                s2 += dR * dR;
+            }
+            const double d2 = sqrt(s2) * INV_SQRT18 / h0;
             double h1;
             if (d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
             else h1 = pow(0.01 / fmax(d1, d2), 0.2);
@@ -310,45 +368,90 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
         const double h = tnew - t;
         ha = fabs(h);
 
-        double K1[NS], K2[NS], K3[NS], K4[NS], K5[NS], K6[NS], yt[NS];
+        // f's implied parts: alpha' = masked u_z(y), r' = R(y) e3
+        double fr[3] = {yR[2], yR[5], yR[8]};
+        // B / E accumulators for r (never an RHS input)
+        double br[3], er[3];
         #pragma unroll
-        for (int i = 0; i < NS; ++i) yt[i] = y[i] + (f[i] * A10) * h;
-        rhs<HAS_UY>(p, yt, K1);
+        for (int i = 0; i < 3; ++i) { br[i] = fr[i] * B0; er[i] = fr[i] * E0; }
+
+        Stage K1, K2, K3, K4, K5;
+        double ui[3], ai[3], Ri[9], rc[3];
+#define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF)                                  \
+        {                                                                                      \
+            _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
+                ui[i] = yu[i] + (EXPR_U) * h;                                                  \
+                ai[i] = ya[i] + (EXPR_A) * h;                                                  \
+            }                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = yR[i] + (EXPR_R) * h;        \
+            const Trig tt = trig_of(ai);                                                       \
+            rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
+            stage_at(p, tt, ui, Ri, KOUT, rc);                                                 \
+            _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
+                br[i] += rc[i] * (BCOEF);                                                      \
+                er[i] += rc[i] * (ECOEF);                                                      \
+            }                                                                                  \
+        }
+        CTR_STAGE(K1, f.uz[i] * A10, f.al[i] * A10, f.R[i] * A10, 0.0, 0.0)
+        CTR_STAGE(K2, f.uz[i] * A20 + K1.uz[i] * A21, f.al[i] * A20 + K1.al[i] * A21,
+                  f.R[i] * A20 + K1.R[i] * A21, B2, E2)
+        CTR_STAGE(K3, f.uz[i] * A30 + K1.uz[i] * A31 + K2.uz[i] * A32,
+                  f.al[i] * A30 + K1.al[i] * A31 + K2.al[i] * A32,
+                  f.R[i] * A30 + K1.R[i] * A31 + K2.R[i] * A32, B3, E3)
+        CTR_STAGE(K4, f.uz[i] * A40 + K1.uz[i] * A41 + K2.uz[i] * A42 + K3.uz[i] * A43,
+                  f.al[i] * A40 + K1.al[i] * A41 + K2.al[i] * A42 + K3.al[i] * A43,
+                  f.R[i] * A40 + K1.R[i] * A41 + K2.R[i] * A42 + K3.R[i] * A43, B4, E4)
+        CTR_STAGE(K5, f.uz[i] * A50 + K1.uz[i] * A51 + K2.uz[i] * A52 + K3.uz[i] * A53 + K4.uz[i] * A54,
+                  f.al[i] * A50 + K1.al[i] * A51 + K2.al[i] * A52 + K3.al[i] * A53 + K4.al[i] * A54,
+                  f.R[i] * A50 + K1.R[i] * A51 + K2.R[i] * A52 + K3.R[i] * A53 + K4.R[i] * A54, B5, E5)
+#undef CTR_STAGE
+        // y_new (rk.py rk_step) and the error sums without K6
+        double nu[3], na[3], nr[3], nR[9];
+        double eu[3], ea[3], eR[9];
         #pragma unroll
-        for (int i = 0; i < NS; ++i) yt[i] = y[i] + (f[i] * A20 + K1[i] * A21) * h;
-        rhs<HAS_UY>(p, yt, K2);
+        for (int i = 0; i < 3; ++i) {
+            nu[i] = yu[i] + h * (f.uz[i] * B0 + K2.uz[i] * B2 + K3.uz[i] * B3 + K4.uz[i] * B4 + K5.uz[i] * B5);
+            na[i] = ya[i] + h * (f.al[i] * B0 + K2.al[i] * B2 + K3.al[i] * B3 + K4.al[i] * B4 + K5.al[i] * B5);
+            nr[i] = yr[i] + h * br[i];
+            eu[i] = f.uz[i] * E0 + K2.uz[i] * E2 + K3.uz[i] * E3 + K4.uz[i] * E4 + K5.uz[i] * E5;
+            ea[i] = f.al[i] * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5;
+        }
         #pragma unroll
-        for (int i = 0; i < NS; ++i) yt[i] = y[i] + (f[i] * A30 + K1[i] * A31 + K2[i] * A32) * h;
-        rhs<HAS_UY>(p, yt, K3);
-        #pragma unroll
-        for (int i = 0; i < NS; ++i)
-            yt[i] = y[i] + (f[i] * A40 + K1[i] * A41 + K2[i] * A42 + K3[i] * A43) * h;
-        rhs<HAS_UY>(p, yt, K4);
-        #pragma unroll
-        for (int i = 0; i < NS; ++i)
-            yt[i] = y[i] + (f[i] * A50 + K1[i] * A51 + K2[i] * A52 + K3[i] * A53 + K4[i] * A54) * h;
-        rhs<HAS_UY>(p, yt, K5);
-        double ynew[NS];
-        #pragma unroll
-        for (int i = 0; i < NS; ++i)
-            ynew[i] = y[i] + h * (f[i] * B0 + K2[i] * B2 + K3[i] * B3 + K4[i] * B4 + K5[i] * B5);
-        rhs<HAS_UY>(p, ynew, K6);
+        for (int i = 0; i < 9; ++i) {
+            nR[i] = yR[i] + h * (f.R[i] * B0 + K2.R[i] * B2 + K3.R[i] * B3 + K4.R[i] * B4 + K5.R[i] * B5);
+            eR[i] = f.R[i] * E0 + K2.R[i] * E2 + K3.R[i] * E3 + K4.R[i] * E4 + K5.R[i] * E5;
+        }
+        Stage K6;
+        double k6r[3];
+        const Trig tn = trig_of(na);
+        rhs_core<HAS_UY>(p, tn, nu, nR, K6.uz, K6.R);
+        stage_at(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
+        // error norm: RMS of h * (K^T E) / (atol + max(|y|, |y_new|) rtol)
         double en2 = 0.0;
         #pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const double scale = ATOL + fmax(fabs(y[i]), fabs(ynew[i])) * RTOL;
-            const double e = ((f[i] * E0 + K2[i] * E2 + K3[i] * E3 + K4[i] * E4 + K5[i] * E5 + K6[i] * E6) * h)
-                             / scale;
-            en2 += e * e;
+        for (int i = 0; i < 3; ++i) {
+            const double xu = ((eu[i] + K6.uz[i] * E6) * h) / (ATOL + fmax(fabs(yu[i]), fabs(nu[i])) * RTOL);
+            const double xa = ((ea[i] + K6.al[i] * E6) * h) / (ATOL + fmax(fabs(ya[i]), fabs(na[i])) * RTOL);
+            const double xr = ((er[i] + k6r[i] * E6) * h) / (ATOL + fmax(fabs(yr[i]), fabs(nr[i])) * RTOL);
+            en2 += xu * xu + xa * xa + xr * xr;
         }
-        const double en = sqrt(en2) * 0.23570226039551584;
+        #pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double xR = ((eR[i] + K6.R[i] * E6) * h) / (ATOL + fmax(fabs(yR[i]), fabs(nR[i])) * RTOL);
+            en2 += xR * xR;
+        }
+        const double en = sqrt(en2) * INV_SQRT18;
         if (en < 1.0) {
             double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * pow(en, -0.2));
             if (rejected) factor = fmin(1.0, factor);
             ha *= factor;
             #pragma unroll
-            for (int i = 0; i < NS; ++i) { y[i] = ynew[i]; f[i] = K6[i]; }
+            for (int i = 0; i < 3; ++i) { yu[i] = nu[i]; ya[i] = na[i]; yr[i] = nr[i]; }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) yR[i] = nR[i];
+            f = K6;
+            ty = tn;
             t = tnew;
             st.nstep++;
             new_step = true;
@@ -359,7 +462,7 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             st.nrej++;
         }
     }
-    tip[0] = y[6]; tip[1] = y[7]; tip[2] = y[8];
+    tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 }
 

@@ -189,7 +189,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
 }
 
 // ------------------------------------------------------------------------------------------
-// Reset.  mode 0: envs from the work list (count in work[0]); mode 1: all envs with mask.
+// Reset.  Two lanes per environment: the even lane draws the desired joints and runs the goal
+// FK (ctr_reach_env.py:100-101), the odd lane draws the start joints and runs the start FK
+// (:104-112); the pair then swaps results with a lane shuffle and the odd lane writes the env.
+// mode 0: envs from the auto-reset work list (count in work[0]); mode 1: all envs (or mask).
 template <bool HAS_UY>
 __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mode, const uint8_t *__restrict__ mask,
                                                     const double *__restrict__ goal,
@@ -200,73 +203,80 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
     __shared__ int s_count;
     if (mode == 0 && threadIdx.x == 0) s_count = b.work[0];
     stage_systems(kc, s_sys);
-    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    int64_t e;
+    const int64_t slot = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 1;
+    const bool odd = threadIdx.x & 1;
+    int64_t e = -1;
     if (mode == 0) {
-        if (i >= s_count) return;
-        e = b.work[1 + i];
-    } else {
-        if (i >= b.n) return;
-        if (mask && !mask[i]) return;
-        e = i;
+        if (slot < s_count) e = b.work[1 + slot];
+    } else if (slot < b.n && (!mask || mask[slot])) {
+        e = slot;
     }
-    const uint64_t genv = (uint64_t)(b.env_base + e);
-    const uint32_t epoch = b.epoch[e] + 1;           // reset number of this reset
-    b.epoch[e] = epoch;
+    const bool active = e >= 0;
+    const uint64_t genv = (uint64_t)(b.env_base + (active ? e : 0));
+    const uint32_t epoch = active ? b.epoch[e] + 1 : 0;        // reset number of this reset
     const uint64_t seed = kc.c.seed;
     const int ns = kc.c.n_systems;
-    const int s = sys_in ? clamp_sys(sys_in[e], ns) : sample_system(seed, epoch, genv, ns);
+    const int s = !active ? 0 : sys_in ? clamp_sys(sys_in[e], ns) : sample_system(seed, epoch, genv, ns);
     const ctr_system_t &sy = s_sys[s];
     uint32_t stat = 0;
-    double dg[3];
-    float qd[6];
-    if (goal) {
-        #pragma unroll
-        for (int k = 0; k < 3; ++k) dg[k] = goal[3 * e + k];
-        #pragma unroll
-        for (int k = 0; k < 6; ++k) qd[k] = 0.0f;
-    } else {
-        if (sample_joints_lane(sy, seed, epoch, 0u, genv, qd) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
-        FkStats st = {0, 0, 0, 0, 0};
-        fk_dispatch<HAS_UY>(sy, qd, dg, st);                      // ctr_reach_env.py:101
-        stat |= st.status;
+    float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    double tip[3] = {0.0, 0.0, 0.0};
+    if (active) {
+        const bool sample = odd ? (kc.c.resample_joints != 0) : (goal == nullptr);
+        if (sample) {
+            if (sample_joints_lane(sy, seed, epoch, odd ? 1u : 0u, genv, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
+        } else if (odd) {
+            #pragma unroll
+            for (int k = 0; k < 6; ++k) qv[k] = b.joints[6 * e + k];
+        }
+        if (!odd && goal) {
+            #pragma unroll
+            for (int k = 0; k < 3; ++k) tip[k] = goal[3 * e + k];
+        } else {
+            FkStats st = {0, 0, 0, 0, 0};
+            fk_dispatch<HAS_UY>(sy, qv, tip, st);                 // :101 (even) / :108, :112 (odd)
+            stat |= st.status;
+        }
     }
-    float q0[6];
-    if (kc.c.resample_joints) {
-        if (sample_joints_lane(sy, seed, epoch, 1u, genv, q0) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
-    } else {
-        #pragma unroll
-        for (int k = 0; k < 6; ++k) q0[k] = b.joints[6 * e + k];
-    }
-    double ag[3];
-    {
-        FkStats st = {0, 0, 0, 0, 0};
-        fk_dispatch<HAS_UY>(sy, q0, ag, st);                      // :108 / :112
-        stat |= st.status;
-    }
+    // exchange within the pair (all lanes of the wave are converged here)
+    double other[3];
     #pragma unroll
-    for (int k = 0; k < 6; ++k) b.joints[6 * e + k] = q0[k];
+    for (int k = 0; k < 3; ++k) other[k] = __shfl_xor(tip[k], 1);
+    float qother[6];
+    #pragma unroll
+    for (int k = 0; k < 6; ++k) qother[k] = __shfl_xor(qv[k], 1);
+    const uint32_t stat_other = __shfl_xor(stat, 1);
+    if (!active) return;
+    if (!odd) {
+        if (b.desired_joints)
+            #pragma unroll
+            for (int k = 0; k < 6; ++k) b.desired_joints[6 * e + k] = qv[k];
+        return;
+    }
+    const double *dg = other;        // from the even lane
+    const double *ag = tip;
+    (void)qother;
+    #pragma unroll
+    for (int k = 0; k < 6; ++k) b.joints[6 * e + k] = qv[k];
     #pragma unroll
     for (int k = 0; k < 3; ++k) { b.desired_goal[3 * e + k] = dg[k]; b.achieved_goal[3 * e + k] = ag[k]; }
     b.t[e] = 0;
     b.system[e] = s;
-    if (b.desired_joints)
-        #pragma unroll
-        for (int k = 0; k < 6; ++k) b.desired_joints[6 * e + k] = qd[k];
+    b.epoch[e] = epoch;
     if (b.starting_joints)
         #pragma unroll
-        for (int k = 0; k < 6; ++k) b.starting_joints[6 * e + k] = q0[k];
+        for (int k = 0; k < 6; ++k) b.starting_joints[6 * e + k] = qv[k];
     if (b.starting_position)
         #pragma unroll
         for (int k = 0; k < 3; ++k) b.starting_position[3 * e + k] = ag[k];
     const bool multi = ns > 1;
     const int od = multi ? 14 : 13;
     float ob[14];
-    obs_lane(q0, dg, ag, kc.c.tol, s, multi, kc.c.egocentric != 0, ob);   // :114
+    obs_lane(qv, dg, ag, kc.c.tol, s, multi, kc.c.egocentric != 0, ob);   // :114
     #pragma unroll
     for (int k = 0; k < 13; ++k) obs[od * e + k] = ob[k];
     if (multi) obs[od * e + 13] = ob[13];
-    if (status) status[e] |= stat;
+    if (status) status[e] |= stat | stat_other;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_clear_work(int32_t *work)
@@ -355,7 +365,7 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (autoreset && !b.work) return fail(CTR_EINVAL, "ctr_step: autoreset needs batch->work");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = grid_for(b.n);
+    const unsigned g = grid_for(b.n), g2 = grid_for(2 * b.n);
     if (autoreset) hipLaunchKernelGGL(k_clear_work, dim3(1), dim3(64), 0, s, b.work);
     if (kc.has_uy)
         hipLaunchKernelGGL(k_step<true>, dim3(g), dim3(BLOCK), 0, s, kc, b, actions, o, autoreset);
@@ -364,10 +374,10 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset) {
         if (kc.has_uy)
-            hipLaunchKernelGGL(k_reset<true>, dim3(g), dim3(BLOCK), 0, s, kc, b, 0, nullptr, nullptr, nullptr, o.obs,
+            hipLaunchKernelGGL(k_reset<true>, dim3(g2), dim3(BLOCK), 0, s, kc, b, 0, nullptr, nullptr, nullptr, o.obs,
                                o.status);
         else
-            hipLaunchKernelGGL(k_reset<false>, dim3(g), dim3(BLOCK), 0, s, kc, b, 0, nullptr, nullptr, nullptr, o.obs,
+            hipLaunchKernelGGL(k_reset<false>, dim3(g2), dim3(BLOCK), 0, s, kc, b, 0, nullptr, nullptr, nullptr, o.obs,
                                o.status);
         return hip_check("ctr_step reset launch");
     }
@@ -387,10 +397,10 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
     if (kc.has_uy)
-        hipLaunchKernelGGL(k_reset<true>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, kc, b, 1, mask, goal, system, obs,
+        hipLaunchKernelGGL(k_reset<true>, dim3(grid_for(2 * b.n)), dim3(BLOCK), 0, s, kc, b, 1, mask, goal, system, obs,
                            status);
     else
-        hipLaunchKernelGGL(k_reset<false>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, kc, b, 1, mask, goal, system, obs,
+        hipLaunchKernelGGL(k_reset<false>, dim3(grid_for(2 * b.n)), dim3(BLOCK), 0, s, kc, b, 1, mask, goal, system, obs,
                            status);
     return hip_check("ctr_reset launch");
 }

@@ -1,0 +1,52 @@
+// ctr_math.hpp -- fp64 elementary functions for the CTR kernels (host + device).
+//
+// sincos_cw: Cody-Waite reduction by pi/2 (three FMA terms) + fdlibm-style minimax kernels on
+// [-pi/4, pi/4]; sine and cosine share one reduction.  Arguments beyond |x| < 2^20 (never
+// reached by joint angles, which are bounded by the action limits and episode length) fall
+// back to the math library.  Max error <= 2 ulp is checked on the host by tests/test_math.py.
+#pragma once
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define CTR_HD __host__ __device__ __forceinline__
+#else
+#define CTR_HD static inline
+#endif
+
+namespace ctr_math {
+
+CTR_HD void sincos_cw(double x, double *sp, double *cp)
+{
+    if (!(fabs(x) < 1048576.0)) {                 // rare: huge or non-finite arguments
+        *sp = sin(x);
+        *cp = cos(x);
+        return;
+    }
+    const double n = rint(x * 0.6366197723675814);             // round(x * 2/pi)
+    double r = fma(-n, 1.5707963267948966, x);                 // pi/2 = P1 + P2 + P3
+    r = fma(-n, 6.123233995736766e-17, r);
+    r = fma(-n, -1.4973849048591698e-33, r);
+    const double z = r * r;
+    // sin kernel (|r| <= pi/4)
+    const double ps = 8.33333333332248946124e-03 +
+                      z * (-1.98412698298579493134e-04 +
+                           z * (2.75573137070700676789e-06 +
+                                z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+    const double s = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
+    // cos kernel
+    const double pc = z * (4.16666666666666019037e-02 +
+                           z * (-1.38888888888741095749e-03 +
+                                z * (2.48015872894767294178e-05 +
+                                     z * (-2.75573143513906633035e-07 +
+                                          z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * pc);
+    const int q = ((int)n) & 3;
+    const double ss = (q & 1) ? c : s;
+    const double cc = (q & 1) ? s : c;
+    *sp = (q & 2) ? -ss : ss;
+    *cp = ((q + 1) & 2) ? -cc : cc;
+}
+
+}  // namespace ctr_math

@@ -1,0 +1,19 @@
+#!/bin/bash
+# rocprofv3 kernel-trace stats + PMC passes for bench.py (run on the GPU box).
+# usage: bash scripts/profile.sh <tag>
+set -o pipefail
+TAG=${1:-r01}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+    python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline > $OUT/bench_under_trace.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc1.log 2>&1 || exit 2
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc2.log 2>&1 || exit 3
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_valu -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc3.log 2>&1 || exit 4
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/pmc_f64 -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc4.log 2>&1 || echo "pmc4 failed (counter names?)"
+find $OUT -name "*.csv" | head -50

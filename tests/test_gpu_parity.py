@@ -108,8 +108,9 @@ def test_set_action_bit_exact_vs_oracle(cuda, oracle_mod):
         q[:, 3:] = rng.uniform(-3.3, 3.3, (n, 3)).astype(np.float32)
         a = (rng.choice([-1, 1], (n, 6)) * rng.uniform(0.2, 1.0, (n, 6)) * env.action_space.high).astype(np.float32)
         qd = torch.tensor(q, device=cuda)
-        rc = env.lib.ctr_set_action(env.cfg, _abi.ptr(qd), _abi.ptr(torch.tensor(sysid, device=cuda)),
-                                    _abi.ptr(torch.tensor(a, device=cuda)), n, _abi.stream_ptr())
+        sd = torch.tensor(sysid, device=cuda)      # keep the tensors alive across the async launch
+        ad = torch.tensor(a, device=cuda)
+        rc = env.lib.ctr_set_action(env.cfg, _abi.ptr(qd), _abi.ptr(sd), _abi.ptr(ad), n, _abi.stream_ptr())
         _abi.check(rc, "ctr_set_action")
         ref = oracle_mod.set_action(q, a, system=sysid, systems=oracle_mod.make_systems(), constrain_alpha=ca)
         np.testing.assert_array_equal(qd.cpu().numpy(), ref)
@@ -146,6 +147,7 @@ def test_autoreset_and_terminal_obs(cuda):
     import torch
     n = 2048
     env = _env(cuda, n, seed=5, max_steps_per_episode=3)
+    env.goal_tolerance.current_tol = 1e-12      # no early success: every episode ends by time limit
     env.reset()
     a = torch.zeros((n, 6), device=cuda)
     for k in range(3):
@@ -155,8 +157,11 @@ def test_autoreset_and_terminal_obs(cuda):
     assert (env.t.cpu().numpy() == 0).all()     # ... and every env was reset in the same call
     assert (env.epoch.cpu().numpy() == 2).all()
     term = info["terminal_observation"].cpu().numpy()
-    np.testing.assert_allclose(term[:, 9:12], (env.desired_goal.cpu().numpy() * 0 + term[:, 9:12]))
-    assert not np.allclose(term, obs["observation"].cpu().numpy())
+    assert (term[:, 12] == np.float32(env.get_goal_tolerance())).all()
+    # the returned observation is the new episode's: its goal offset is dg' - FK(q0')
+    new = obs["observation"].cpu().numpy()
+    np.testing.assert_allclose(new[:, 9:12], (env.desired_goal - env.achieved_goal).cpu().numpy(), atol=1e-6)
+    assert (np.abs(term[:, 9:12] - new[:, 9:12]).max(axis=1) > 0).mean() > 0.99
 
 
 def test_shard_invariance(cuda):
