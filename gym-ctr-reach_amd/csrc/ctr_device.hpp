@@ -295,12 +295,12 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             double isc_u[3], isc_a[3], isc_r[3], isc_R[9];
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                isc_u[i] = 1.0 / (ATOL + fabs(yu[i]) * RTOL);
-                isc_a[i] = 1.0 / (ATOL + fabs(ya[i]) * RTOL);
-                isc_r[i] = 1.0 / (ATOL + fabs(yr[i]) * RTOL);
+                isc_u[i] = ctr_math::rcp(ATOL + fabs(yu[i]) * RTOL);
+                isc_a[i] = ctr_math::rcp(ATOL + fabs(ya[i]) * RTOL);
+                isc_r[i] = ctr_math::rcp(ATOL + fabs(yr[i]) * RTOL);
             }
             #pragma unroll
-            for (int i = 0; i < 9; ++i) isc_R[i] = 1.0 / (ATOL + fabs(yR[i]) * RTOL);
+            for (int i = 0; i < 9; ++i) isc_R[i] = ctr_math::rcp(ATOL + fabs(yR[i]) * RTOL);
             double s0 = 0.0, s1 = 0.0;
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -345,7 +345,7 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             const double d2 = sqrt(s2) * INV_SQRT18 / h0;
             double h1;
             if (d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
-            else h1 = pow(0.01 / fmax(d1, d2), 0.2);
+            else h1 = ctr_math::powpos(0.01 / fmax(d1, d2), 0.2);
             ha = fmin(fmin(100.0 * h0, h1), interval);
             t = t0;
             need_init = false;
@@ -431,19 +431,19 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
         double en2 = 0.0;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double xu = ((eu[i] + K6.uz[i] * E6) * h) / (ATOL + fmax(fabs(yu[i]), fabs(nu[i])) * RTOL);
-            const double xa = ((ea[i] + K6.al[i] * E6) * h) / (ATOL + fmax(fabs(ya[i]), fabs(na[i])) * RTOL);
-            const double xr = ((er[i] + k6r[i] * E6) * h) / (ATOL + fmax(fabs(yr[i]), fabs(nr[i])) * RTOL);
+            const double xu = ((eu[i] + K6.uz[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(yu[i]), fabs(nu[i])) * RTOL);
+            const double xa = ((ea[i] + K6.al[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(ya[i]), fabs(na[i])) * RTOL);
+            const double xr = ((er[i] + k6r[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(yr[i]), fabs(nr[i])) * RTOL);
             en2 += xu * xu + xa * xa + xr * xr;
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const double xR = ((eR[i] + K6.R[i] * E6) * h) / (ATOL + fmax(fabs(yR[i]), fabs(nR[i])) * RTOL);
+            const double xR = ((eR[i] + K6.R[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(yR[i]), fabs(nR[i])) * RTOL);
             en2 += xR * xR;
         }
         const double en = sqrt(en2) * INV_SQRT18;
         if (en < 1.0) {
-            double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * pow(en, -0.2));
+            double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * ctr_math::powpos(en, -0.2));
             if (rejected) factor = fmin(1.0, factor);
             ha *= factor;
             #pragma unroll
@@ -457,7 +457,7 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             new_step = true;
             if (t - tb >= 0.0) need_init = true;    // segment finished (status 'finished')
         } else {
-            ha *= fmax(0.2, 0.9 * pow(en, -0.2));
+            ha *= fmax(0.2, 0.9 * ctr_math::powpos(en, -0.2));
             rejected = true;
             st.nrej++;
         }

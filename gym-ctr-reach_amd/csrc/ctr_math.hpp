@@ -15,11 +15,23 @@
 
 namespace ctr_math {
 
+// Out-of-line slow path (keeps the math library's large-argument reduction out of every
+// inlined call site).
+#if defined(__HIPCC__)
+__host__ __device__ __attribute__((noinline))
+#else
+static
+#endif
+void sincos_slow(double x, double *sp, double *cp)
+{
+    *sp = sin(x);
+    *cp = cos(x);
+}
+
 CTR_HD void sincos_cw(double x, double *sp, double *cp)
 {
     if (!(fabs(x) < 1048576.0)) {                 // rare: huge or non-finite arguments
-        *sp = sin(x);
-        *cp = cos(x);
+        sincos_slow(x, sp, cp);
         return;
     }
     const double n = rint(x * 0.6366197723675814);             // round(x * 2/pi)
@@ -47,6 +59,26 @@ CTR_HD void sincos_cw(double x, double *sp, double *cp)
     const double cc = (q & 1) ? s : c;
     *sp = (q & 2) ? -ss : ss;
     *cp = ((q + 1) & 2) ? -cc : cc;
+}
+
+// 1/x to within 1 ulp: hardware reciprocal estimate + two Newton-Raphson steps.
+CTR_HD double rcp(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+
+// x^y for x > 0 through exp2/log2 (step-size factors only; a few ulp).
+CTR_HD double powpos(double x, double y)
+{
+    return exp2(y * log2(x));
 }
 
 }  // namespace ctr_math
