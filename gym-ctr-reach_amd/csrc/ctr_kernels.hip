@@ -1,16 +1,18 @@
 // ctr_kernels.hip -- HIP kernels + the extern "C" ABI of libctr_reach_amd.so (gfx950).
 //
-// Kernels (one environment per lane, 256-lane workgroups):
+// Kernels (one environment per lane unless stated, 256-lane workgroups):
 //   k_fk          Model.forward_kinematics for a batch                 (envs/model.py:30-70)
 //   k_set_action  n_substeps x Obs.set_action                          (envs/obs.py:166-183)
 //   k_step        fused CtrReachEnv.step: set_action x n_substeps, FK, reward, done,
-//                 success, error, observation; appends done envs to a reset work list
-//                 with one wave-aggregated atomic per wave          (envs/ctr_reach_env.py:124-158)
-//   k_reset       CtrReachEnv.reset for listed / masked envs: system pick, two
-//                 sample_goal draws (Philox), two FKs, observation   (envs/ctr_reach_env.py:70-114)
+//                 success, error, observation; a done env takes its next reset from the
+//                 reset pool (a copy), or is queued for k_reset      (envs/ctr_reach_env.py:124-158)
+//   k_reset       CtrReachEnv.reset, TWO lanes per env (goal FK | start FK in parallel),
+//                 for the queued / masked envs                        (envs/ctr_reach_env.py:70-114)
+//   k_refill      precomputes queued resets into the pool, two lanes per reset
 //   k_reward      compute_reward over a batch                          (envs/ctr_reach_env.py:160-170)
 //
-// The tube tables (<= 8 systems x 18 doubles) travel as a kernel argument and are staged
+// Work lists (auto-reset misses, pool refills) are appended with one wave-aggregated atomic per
+// wave.  The tube tables (<= 8 systems x 18 doubles) travel as a kernel argument and are staged
 // once per workgroup into LDS; every lane then reads its system's row from LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -65,6 +67,31 @@ template <bool HAS_UY>
 __device__ __forceinline__ void fk_dispatch(const ctr_system_t &sy, const float q[6], double tip[3], FkStats &st)
 {
     fk_lane<HAS_UY>(sy, q, tip, st);
+}
+
+// Wave-aggregated append of `n_items` int32 per active lane to list (count at list[0]).
+__device__ __forceinline__ void wave_append(int32_t *list, int64_t cap, bool active, const int32_t *items,
+                                            int n_items)
+{
+    const uint64_t m = __ballot(active);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(m);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&list[0], __popcll(m));
+    base = __shfl(base, leader);
+    if (active) {
+        const int64_t slot = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (slot < cap)
+            for (int k = 0; k < n_items; ++k) list[1 + n_items * slot + k] = items[k];
+    }
+}
+
+__device__ __forceinline__ void write_obs(float *dst, const float ob[14], bool multi)
+{
+    #pragma unroll
+    for (int k = 0; k < 13; ++k) dst[k] = ob[k];
+    if (multi) dst[13] = ob[13];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -122,7 +149,9 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
     stage_systems(kc, s_sys);
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool live = e < b.n;
-    bool done = false;
+    bool miss = false;       // done, but no pooled reset available -> k_reset
+    bool pooled = false;     // done and reset from the pool -> queue the refill
+    uint32_t pooled_r = 0;
     if (live) {
         const int s = clamp_sys(b.system[e], kc.c.n_systems);
         const ctr_system_t &sy = s_sys[s];
@@ -141,58 +170,134 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
         const double d = sqrt(dx * dx + dy * dy + dz * dz);
         const double tol = kc.c.tol;
         const float reward = (d > tol) ? -1.0f : 0.0f;              // ctr_reach_env.py:170
-        done = (reward == 0.0f) || (t >= kc.c.max_steps);           // :140
+        const bool done = (reward == 0.0f) || (t >= kc.c.max_steps); // :140
         const bool multi = kc.c.n_systems > 1;
         const int od = multi ? 14 : 13;
         float obs[14];
         obs_lane(q, dg, ag, tol, s, multi, kc.c.egocentric != 0, obs);
-        #pragma unroll
-        for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = q[i];
-        #pragma unroll
-        for (int i = 0; i < 3; ++i) b.achieved_goal[3 * e + i] = ag[i];
-        b.t[e] = t;
-        #pragma unroll
-        for (int i = 0; i < 13; ++i) o.obs[od * e + i] = obs[i];
-        if (multi) o.obs[od * e + 13] = obs[13];
         o.reward[e] = reward;
         o.done[e] = done ? 1 : 0;
         o.success[e] = (d < tol) ? 1 : 0;                           // :155
         o.error[e] = (float)d;
-        if (o.status) o.status[e] = st.status;
+        uint32_t stat = st.status;
         if (o.nfev) o.nfev[e] = st.nfev;
+        int32_t t_out = t;
         if (autoreset && done) {
-            if (o.terminal_obs) {
-                #pragma unroll
-                for (int i = 0; i < 13; ++i) o.terminal_obs[od * e + i] = obs[i];
-                if (multi) o.terminal_obs[od * e + 13] = obs[13];
-            }
+            if (o.terminal_obs) write_obs(o.terminal_obs + od * e, obs, multi);
             if (o.terminal_achieved)
                 #pragma unroll
                 for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
+            const uint32_t r = b.epoch[e] + 1;                      // reset number to take
+            const int P = b.pool_depth;
+            const int64_t ps = P > 0 ? (int64_t)(r % (uint32_t)P) * b.n + e : 0;
+            if (P > 0 && b.pool_r[ps] == r) {
+                // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
+                const int s2 = clamp_sys(b.pool_sys[ps], kc.c.n_systems);
+                #pragma unroll
+                for (int i = 0; i < 6; ++i) q[i] = b.pool_q0[6 * ps + i];
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) { dg[i] = b.pool_dg[3 * ps + i]; ag[i] = b.pool_ag[3 * ps + i]; }
+                if (b.desired_joints)
+                    #pragma unroll
+                    for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = b.pool_qd[6 * ps + i];
+                if (b.starting_joints)
+                    #pragma unroll
+                    for (int i = 0; i < 6; ++i) b.starting_joints[6 * e + i] = q[i];
+                if (b.starting_position)
+                    #pragma unroll
+                    for (int i = 0; i < 3; ++i) b.starting_position[3 * e + i] = ag[i];
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) b.desired_goal[3 * e + i] = dg[i];
+                b.system[e] = s2;
+                b.epoch[e] = r;
+                stat |= b.pool_stat[ps];
+                obs_lane(q, dg, ag, kc.c.tol, s2, multi, kc.c.egocentric != 0, obs);
+                pooled = true;
+                pooled_r = r;
+                t_out = 0;
+            } else {
+                miss = true;
+            }
         }
+        b.t[e] = t_out;
+        #pragma unroll
+        for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = q[i];
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) b.achieved_goal[3 * e + i] = ag[i];
+        write_obs(o.obs + od * e, obs, multi);
+        if (o.status) o.status[e] = stat;
     }
     if (autoreset) {
-        // wave-aggregated append of done envs to the reset list b.work[1 + slot]
-        const uint64_t m = __ballot(live && done);
-        if (m) {
-            const int lane = threadIdx.x & 63;
-            const int leader = __builtin_ctzll(m);
-            int base = 0;
-            if (lane == leader) base = atomicAdd(&b.work[0], __popcll(m));
-            base = __shfl(base, leader);
-            if (live && done) {
-                const int off = __popcll(m & ((1ull << lane) - 1ull));
-                b.work[1 + base + off] = (int32_t)e;
-            }
+        const int32_t one[1] = {(int32_t)e};
+        wave_append(b.work, b.n, miss, one, 1);
+        if (b.pool_depth > 0) {
+            const int32_t two[2] = {(int32_t)e, (int32_t)(pooled_r + (uint32_t)b.pool_depth)};
+            wave_append(b.refill, b.refill_cap, pooled, two, 2);
         }
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// Reset.  Two lanes per environment: the even lane draws the desired joints and runs the goal
-// FK (ctr_reach_env.py:100-101), the odd lane draws the start joints and runs the start FK
-// (:104-112); the pair then swaps results with a lane shuffle and the odd lane writes the env.
-// mode 0: envs from the auto-reset work list (count in work[0]); mode 1: all envs (or mask).
+// One reset (reset number r of global env genv) computed by a lane PAIR: the even lane draws the
+// desired joints and runs the goal FK (ctr_reach_env.py:100-101), the odd lane draws the start
+// joints and runs the start FK (:104-112); results are swapped with lane shuffles.  Every lane
+// of the wave must call this (inactive lanes with active = false).
+struct ResetOut {
+    float qd[6], q0[6];
+    double dg[3], ag[3];
+    int sys;
+    uint32_t stat;
+};
+
+template <bool HAS_UY>
+__device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const ctr_system_t *s_sys, bool active, bool odd,
+                                               uint64_t genv, uint32_t r, const float *q_cur, const double *goal,
+                                               int sys_fixed)
+{
+    const uint64_t seed = kc.c.seed;
+    const int ns = kc.c.n_systems;
+    const int s = !active ? 0 : (sys_fixed >= 0 ? sys_fixed : sample_system(seed, r, genv, ns));
+    const ctr_system_t &sy = s_sys[s];
+    uint32_t stat = 0;
+    float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    double tip[3] = {0.0, 0.0, 0.0};
+    if (active) {
+        const bool sample = odd ? (kc.c.resample_joints != 0) : (goal == nullptr);
+        if (sample) {
+            if (sample_joints_lane(sy, seed, r, odd ? 1u : 0u, genv, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
+        } else if (odd) {
+            #pragma unroll
+            for (int k = 0; k < 6; ++k) qv[k] = q_cur[k];
+        }
+        if (!odd && goal) {
+            #pragma unroll
+            for (int k = 0; k < 3; ++k) tip[k] = goal[k];
+        } else {
+            FkStats st = {0, 0, 0, 0, 0};
+            fk_dispatch<HAS_UY>(sy, qv, tip, st);
+            stat |= st.status;
+        }
+    }
+    ResetOut ro;
+    #pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double other = __shfl_xor(tip[k], 1);
+        ro.dg[k] = odd ? other : tip[k];
+        ro.ag[k] = odd ? tip[k] : other;
+    }
+    #pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const float other = __shfl_xor(qv[k], 1);
+        ro.qd[k] = odd ? other : qv[k];
+        ro.q0[k] = odd ? qv[k] : other;
+    }
+    ro.stat = stat | __shfl_xor(stat, 1);
+    ro.sys = s;
+    return ro;
+}
+
+// Synchronous reset.  mode 0: envs queued in b.work by k_step (pool misses / no pool);
+// mode 1: all envs (or mask).  The pair's odd lane writes the env.
 template <bool HAS_UY>
 __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mode, const uint8_t *__restrict__ mask,
                                                     const double *__restrict__ goal,
@@ -201,8 +306,9 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
 {
     __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
     __shared__ int s_count;
-    if (mode == 0 && threadIdx.x == 0) s_count = b.work[0];
+    if (threadIdx.x == 0) s_count = (mode == 0) ? b.work[0] : 0;
     stage_systems(kc, s_sys);
+    if (mode == 0 && (int64_t)blockIdx.x * (BLOCK / 2) >= s_count) return;      // whole block idle
     const int64_t slot = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 1;
     const bool odd = threadIdx.x & 1;
     int64_t e = -1;
@@ -212,76 +318,90 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
         e = slot;
     }
     const bool active = e >= 0;
-    const uint64_t genv = (uint64_t)(b.env_base + (active ? e : 0));
-    const uint32_t epoch = active ? b.epoch[e] + 1 : 0;        // reset number of this reset
-    const uint64_t seed = kc.c.seed;
-    const int ns = kc.c.n_systems;
-    const int s = !active ? 0 : sys_in ? clamp_sys(sys_in[e], ns) : sample_system(seed, epoch, genv, ns);
-    const ctr_system_t &sy = s_sys[s];
-    uint32_t stat = 0;
-    float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    double tip[3] = {0.0, 0.0, 0.0};
-    if (active) {
-        const bool sample = odd ? (kc.c.resample_joints != 0) : (goal == nullptr);
-        if (sample) {
-            if (sample_joints_lane(sy, seed, epoch, odd ? 1u : 0u, genv, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
-        } else if (odd) {
-            #pragma unroll
-            for (int k = 0; k < 6; ++k) qv[k] = b.joints[6 * e + k];
-        }
-        if (!odd && goal) {
-            #pragma unroll
-            for (int k = 0; k < 3; ++k) tip[k] = goal[3 * e + k];
-        } else {
-            FkStats st = {0, 0, 0, 0, 0};
-            fk_dispatch<HAS_UY>(sy, qv, tip, st);                 // :101 (even) / :108, :112 (odd)
-            stat |= st.status;
-        }
-    }
-    // exchange within the pair (all lanes of the wave are converged here)
-    double other[3];
+    const int64_t ee = active ? e : 0;
+    const uint32_t r = active ? b.epoch[ee] + 1 : 0;
+    float qc[6];
     #pragma unroll
-    for (int k = 0; k < 3; ++k) other[k] = __shfl_xor(tip[k], 1);
-    float qother[6];
-    #pragma unroll
-    for (int k = 0; k < 6; ++k) qother[k] = __shfl_xor(qv[k], 1);
-    const uint32_t stat_other = __shfl_xor(stat, 1);
-    if (!active) return;
-    if (!odd) {
+    for (int k = 0; k < 6; ++k) qc[k] = active ? b.joints[6 * ee + k] : 0.f;
+    const int sf = (active && sys_in) ? clamp_sys(sys_in[ee], kc.c.n_systems) : -1;
+    const ResetOut ro = reset_pair<HAS_UY>(kc, s_sys, active, odd, (uint64_t)(b.env_base + ee), r, qc,
+                                           goal ? goal + 3 * ee : nullptr, sf);
+    bool queue = false;
+    if (active && odd) {
+        #pragma unroll
+        for (int k = 0; k < 6; ++k) b.joints[6 * e + k] = ro.q0[k];
+        #pragma unroll
+        for (int k = 0; k < 3; ++k) { b.desired_goal[3 * e + k] = ro.dg[k]; b.achieved_goal[3 * e + k] = ro.ag[k]; }
+        b.t[e] = 0;
+        b.system[e] = ro.sys;
+        b.epoch[e] = r;
         if (b.desired_joints)
             #pragma unroll
-            for (int k = 0; k < 6; ++k) b.desired_joints[6 * e + k] = qv[k];
-        return;
+            for (int k = 0; k < 6; ++k) b.desired_joints[6 * e + k] = ro.qd[k];
+        if (b.starting_joints)
+            #pragma unroll
+            for (int k = 0; k < 6; ++k) b.starting_joints[6 * e + k] = ro.q0[k];
+        if (b.starting_position)
+            #pragma unroll
+            for (int k = 0; k < 3; ++k) b.starting_position[3 * e + k] = ro.ag[k];
+        const bool multi = kc.c.n_systems > 1;
+        float ob[14];
+        obs_lane(ro.q0, ro.dg, ro.ag, kc.c.tol, ro.sys, multi, kc.c.egocentric != 0, ob);   // :114
+        write_obs(obs + (multi ? 14 : 13) * e, ob, multi);
+        if (status) status[e] |= ro.stat;
+        queue = b.pool_depth > 0;
     }
-    const double *dg = other;        // from the even lane
-    const double *ag = tip;
-    (void)qother;
-    #pragma unroll
-    for (int k = 0; k < 6; ++k) b.joints[6 * e + k] = qv[k];
-    #pragma unroll
-    for (int k = 0; k < 3; ++k) { b.desired_goal[3 * e + k] = dg[k]; b.achieved_goal[3 * e + k] = ag[k]; }
-    b.t[e] = 0;
-    b.system[e] = s;
-    b.epoch[e] = epoch;
-    if (b.starting_joints)
-        #pragma unroll
-        for (int k = 0; k < 6; ++k) b.starting_joints[6 * e + k] = qv[k];
-    if (b.starting_position)
-        #pragma unroll
-        for (int k = 0; k < 3; ++k) b.starting_position[3 * e + k] = ag[k];
-    const bool multi = ns > 1;
-    const int od = multi ? 14 : 13;
-    float ob[14];
-    obs_lane(qv, dg, ag, kc.c.tol, s, multi, kc.c.egocentric != 0, ob);   // :114
-    #pragma unroll
-    for (int k = 0; k < 13; ++k) obs[od * e + k] = ob[k];
-    if (multi) obs[od * e + 13] = ob[13];
-    if (status) status[e] |= stat | stat_other;
+    if (b.pool_depth > 0) {
+        // keep the pool P resets deep: mode 0 replaces the reset just taken (r + P); mode 1
+        // (re)queues r+1 .. r+P, skipping slots already holding the right reset
+        if (mode == 0) {
+            const int32_t two[2] = {(int32_t)ee, (int32_t)(r + (uint32_t)b.pool_depth)};
+            wave_append(b.refill, b.refill_cap, queue, two, 2);
+        } else {
+            for (int j = 1; j <= b.pool_depth; ++j) {
+                const uint32_t rr = r + (uint32_t)j;
+                const bool need = queue && b.pool_r[(int64_t)(rr % (uint32_t)b.pool_depth) * b.n + ee] != rr;
+                const int32_t two[2] = {(int32_t)ee, (int32_t)rr};
+                wave_append(b.refill, b.refill_cap, need, two, 2);
+            }
+        }
+    }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_clear_work(int32_t *work)
+// Pool refill: entries (env, reset number) from b.refill, two lanes per entry.
+template <bool HAS_UY>
+__global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) work[0] = 0;
+    __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
+    __shared__ int64_t s_count;
+    if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
+    stage_systems(kc, s_sys);
+    const int64_t per_grid = (int64_t)gridDim.x * (BLOCK / 2);
+    for (int64_t base = (int64_t)blockIdx.x * (BLOCK / 2); base < s_count; base += per_grid) {
+        const int64_t i = base + (threadIdx.x >> 1);
+        const bool odd = threadIdx.x & 1;
+        const bool active = i < s_count;
+        const int64_t e = active ? b.refill[1 + 2 * i] : 0;
+        const uint32_t r = active ? (uint32_t)b.refill[2 + 2 * i] : 0;
+        const int64_t ps = active ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
+        const bool fresh = active && b.pool_r[ps] != r;
+        const ResetOut ro = reset_pair<HAS_UY>(kc, s_sys, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
+                                               nullptr, -1);
+        if (fresh && odd) {
+            #pragma unroll
+            for (int k = 0; k < 6; ++k) { b.pool_qd[6 * ps + k] = ro.qd[k]; b.pool_q0[6 * ps + k] = ro.q0[k]; }
+            #pragma unroll
+            for (int k = 0; k < 3; ++k) { b.pool_dg[3 * ps + k] = ro.dg[k]; b.pool_ag[3 * ps + k] = ro.ag[k]; }
+            b.pool_sys[ps] = ro.sys;
+            b.pool_stat[ps] = ro.stat;
+            b.pool_r[ps] = r;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_clear_counter(int32_t *counter)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) counter[0] = 0;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_reward(const double *__restrict__ ag, const double *__restrict__ dg,
@@ -302,6 +422,19 @@ int check_cfg(const ctr_env_config_t *cfg)
     return 0;
 }
 
+int check_batch(const ctr_batch_t &b, const char *who)
+{
+    if (b.n < 0 || b.n > 0x7fffffff) return fail(CTR_EINVAL, "batch size out of range");
+    if (b.n == 0) return 0;
+    if (!b.joints || !b.desired_goal || !b.achieved_goal || !b.t || !b.system || !b.epoch)
+        return fail(CTR_EINVAL, who);
+    if (b.pool_depth < 0) return fail(CTR_EINVAL, "pool_depth < 0");
+    if (b.pool_depth > 0 && (!b.pool_qd || !b.pool_dg || !b.pool_q0 || !b.pool_ag || !b.pool_sys || !b.pool_r ||
+                             !b.pool_stat || !b.refill || b.refill_cap <= 0))
+        return fail(CTR_EINVAL, "pool_depth > 0 needs every pool buffer and a refill queue");
+    return 0;
+}
+
 KCfg make_kcfg(const ctr_env_config_t *cfg)
 {
     KCfg kc;
@@ -314,6 +447,13 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 }
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
+
+template <typename KT, typename... Args>
+void launch2(bool has_uy, KT kf, KT kt, dim3 g, hipStream_t s, Args... args)
+{
+    if (has_uy) hipLaunchKernelGGL(kt, g, dim3(BLOCK), 0, s, args...);
+    else hipLaunchKernelGGL(kf, g, dim3(BLOCK), 0, s, args...);
+}
 
 }  // namespace
 
@@ -330,11 +470,8 @@ int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env
     if (n < 0 || (n > 0 && (!joints || !tip))) return fail(CTR_EINVAL, "ctr_fk: bad buffers");
     if (n == 0) return 0;
     KCfg kc = make_kcfg(cfg);
-    hipStream_t s = (hipStream_t)stream;
-    if (kc.has_uy)
-        hipLaunchKernelGGL(k_fk<true>, dim3(grid_for(n)), dim3(BLOCK), 0, s, kc, joints, sys_idx, n, tip, stats, status);
-    else
-        hipLaunchKernelGGL(k_fk<false>, dim3(grid_for(n)), dim3(BLOCK), 0, s, kc, joints, sys_idx, n, tip, stats, status);
+    launch2(kc.has_uy != 0, k_fk<false>, k_fk<true>, dim3(grid_for(n)), (hipStream_t)stream, kc, joints, sys_idx, n,
+            tip, stats, status);
     return hip_check("ctr_fk launch");
 }
 
@@ -357,28 +494,19 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (!batch || !out || !actions) return fail(CTR_EINVAL, "ctr_step: NULL argument");
     const ctr_batch_t b = *batch;
     const ctr_step_out_t o = *out;
-    if (b.n < 0) return fail(CTR_EINVAL, "ctr_step: n < 0");
+    if (int r = check_batch(b, "ctr_step: batch buffer missing")) return r;
     if (b.n == 0) return 0;
-    if (!b.joints || !b.desired_goal || !b.achieved_goal || !b.t || !b.system || !b.epoch)
-        return fail(CTR_EINVAL, "ctr_step: batch buffer missing");
     if (!o.obs || !o.reward || !o.done || !o.success || !o.error) return fail(CTR_EINVAL, "ctr_step: output missing");
     if (autoreset && !b.work) return fail(CTR_EINVAL, "ctr_step: autoreset needs batch->work");
+    if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = grid_for(b.n), g2 = grid_for(2 * b.n);
-    if (autoreset) hipLaunchKernelGGL(k_clear_work, dim3(1), dim3(64), 0, s, b.work);
-    if (kc.has_uy)
-        hipLaunchKernelGGL(k_step<true>, dim3(g), dim3(BLOCK), 0, s, kc, b, actions, o, autoreset);
-    else
-        hipLaunchKernelGGL(k_step<false>, dim3(g), dim3(BLOCK), 0, s, kc, b, actions, o, autoreset);
+    if (autoreset) hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.work);
+    launch2(kc.has_uy != 0, k_step<false>, k_step<true>, dim3(grid_for(b.n)), s, kc, b, actions, o, autoreset);
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset) {
-        if (kc.has_uy)
-            hipLaunchKernelGGL(k_reset<true>, dim3(g2), dim3(BLOCK), 0, s, kc, b, 0, nullptr, nullptr, nullptr, o.obs,
-                               o.status);
-        else
-            hipLaunchKernelGGL(k_reset<false>, dim3(g2), dim3(BLOCK), 0, s, kc, b, 0, nullptr, nullptr, nullptr, o.obs,
-                               o.status);
+        launch2(kc.has_uy != 0, k_reset<false>, k_reset<true>, dim3(grid_for(2 * b.n)), s, kc, b, 0,
+                (const uint8_t *)nullptr, (const double *)nullptr, (const int32_t *)nullptr, o.obs, o.status);
         return hip_check("ctr_step reset launch");
     }
     return 0;
@@ -390,19 +518,30 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
     if (int r = check_cfg(cfg)) return r;
     if (!batch || !obs) return fail(CTR_EINVAL, "ctr_reset: NULL argument");
     const ctr_batch_t b = *batch;
-    if (b.n < 0) return fail(CTR_EINVAL, "ctr_reset: n < 0");
+    if (int r = check_batch(b, "ctr_reset: batch buffer missing")) return r;
     if (b.n == 0) return 0;
-    if (!b.joints || !b.desired_goal || !b.achieved_goal || !b.t || !b.system || !b.epoch)
-        return fail(CTR_EINVAL, "ctr_reset: batch buffer missing");
+    if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
+    KCfg kc = make_kcfg(cfg);
+    launch2(kc.has_uy != 0, k_reset<false>, k_reset<true>, dim3(grid_for(2 * b.n)), (hipStream_t)stream, kc, b, 1,
+            mask, goal, system, obs, status);
+    return hip_check("ctr_reset launch");
+}
+
+int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream)
+{
+    if (int r = check_cfg(cfg)) return r;
+    if (!batch) return fail(CTR_EINVAL, "ctr_pool_refill: NULL argument");
+    const ctr_batch_t b = *batch;
+    if (int r = check_batch(b, "ctr_pool_refill: batch buffer missing")) return r;
+    if (b.n == 0 || b.pool_depth == 0) return 0;
+    if (!cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    if (kc.has_uy)
-        hipLaunchKernelGGL(k_reset<true>, dim3(grid_for(2 * b.n)), dim3(BLOCK), 0, s, kc, b, 1, mask, goal, system, obs,
-                           status);
-    else
-        hipLaunchKernelGGL(k_reset<false>, dim3(grid_for(2 * b.n)), dim3(BLOCK), 0, s, kc, b, 1, mask, goal, system, obs,
-                           status);
-    return hip_check("ctr_reset launch");
+    // grid covers one entry per env (2 lanes each); larger queues are swept grid-stride
+    launch2(kc.has_uy != 0, k_refill<false>, k_refill<true>, dim3(grid_for(2 * b.n)), s, kc, b);
+    if (int r = hip_check("ctr_pool_refill launch")) return r;
+    hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.refill);
+    return hip_check("ctr_pool_refill clear");
 }
 
 int ctr_compute_reward(const double *achieved, const double *desired, int64_t n, double tol, float *reward,

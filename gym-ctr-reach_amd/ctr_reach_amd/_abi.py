@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 1
+CTR_ABI_VERSION = 2
 CTR_MAX_SYSTEMS = 8
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1
@@ -56,6 +56,17 @@ class CtrBatch(ctypes.Structure):
         ("starting_joints", _P),
         ("starting_position", _P),
         ("work", _P),
+        ("pool_depth", ctypes.c_int32),
+        ("pool_pad", ctypes.c_int32),
+        ("pool_qd", _P),
+        ("pool_dg", _P),
+        ("pool_q0", _P),
+        ("pool_ag", _P),
+        ("pool_sys", _P),
+        ("pool_r", _P),
+        ("pool_stat", _P),
+        ("refill", _P),
+        ("refill_cap", ctypes.c_int64),
     ]
 
 
@@ -74,7 +85,7 @@ class CtrStepOut(ctypes.Structure):
 
 
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
-            "ctr_compute_reward")
+            "ctr_pool_refill", "ctr_compute_reward")
 
 _lib = None
 
@@ -100,8 +111,9 @@ def load(path=None):
     L.ctr_step.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P,
                            ctypes.POINTER(CtrStepOut), i32, _P]
     L.ctr_reset.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P, _P, _P, _P]
+    L.ctr_pool_refill.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P]
     L.ctr_compute_reward.argtypes = [_P, _P, i64, ctypes.c_double, _P, _P]
-    for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_compute_reward"):
+    for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward"):
         getattr(L, fn).restype = ctypes.c_int
     if L.ctr_abi_version() != CTR_ABI_VERSION:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))

@@ -78,7 +78,8 @@ class CtrReachVecEnv(object):
     plus ``num_envs``, ``device``, ``seed``, ``env_base`` (global id of env 0 for sharding),
     ``autoreset``.  Missing reference kwargs take the CTR-Reach-v0 registration defaults."""
 
-    def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True, **kwargs):
+    def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
+                 pool_depth=None, refill_interval=8, **kwargs):
         torch = _torch()
         kw = default_kwargs()
         kw.update(kwargs)
@@ -139,6 +140,30 @@ class CtrReachVecEnv(object):
         self.terminal_achieved = torch.zeros((n, 3), dtype=f64, device=dev)
         self.status = torch.zeros(n, dtype=i32, device=dev)
         self.nfev = None
+        # reset pool: resets are a pure function of (seed, env id, reset number), so they are
+        # precomputed in batches every `refill_interval` steps and consumed by a copy
+        if pool_depth is None:
+            pool_depth = 4 if (self.autoreset and self.resample_joints) else 0
+        if pool_depth and not self.resample_joints:
+            raise ValueError("the reset pool needs resample_joints=True")
+        self.pool_depth = int(pool_depth)
+        self.refill_interval = max(1, int(refill_interval))
+        self._steps_since_refill = 0
+        P = self.pool_depth
+        if P:
+            self.pool_qd = torch.zeros((P, n, 6), dtype=f32, device=dev)
+            self.pool_dg = torch.zeros((P, n, 3), dtype=f64, device=dev)
+            self.pool_q0 = torch.zeros((P, n, 6), dtype=f32, device=dev)
+            self.pool_ag = torch.zeros((P, n, 3), dtype=f64, device=dev)
+            self.pool_sys = torch.zeros((P, n), dtype=i32, device=dev)
+            self.pool_r = torch.zeros((P, n), dtype=i32, device=dev)
+            self.pool_stat = torch.zeros((P, n), dtype=i32, device=dev)
+            self.refill_cap = n * (P + self.refill_interval)
+            self.refill = torch.zeros(1 + 2 * self.refill_cap, dtype=i32, device=dev)
+        else:
+            self.pool_qd = self.pool_dg = self.pool_q0 = self.pool_ag = None
+            self.pool_sys = self.pool_r = self.pool_stat = self.refill = None
+            self.refill_cap = 0
         self._batch = _abi.CtrBatch()
         self._out = _abi.CtrStepOut()
         self._fill_structs()
@@ -152,6 +177,10 @@ class CtrReachVecEnv(object):
         b.t, b.system, b.epoch, b.work = p(self.t), p(self.system), p(self.epoch), p(self.work)
         b.desired_joints, b.starting_joints = p(self.desired_joints), p(self.starting_joints)
         b.starting_position = p(self.starting_position)
+        b.pool_depth = self.pool_depth
+        b.pool_qd, b.pool_dg, b.pool_q0, b.pool_ag = p(self.pool_qd), p(self.pool_dg), p(self.pool_q0), p(self.pool_ag)
+        b.pool_sys, b.pool_r, b.pool_stat = p(self.pool_sys), p(self.pool_r), p(self.pool_stat)
+        b.refill, b.refill_cap = p(self.refill), self.refill_cap
         o = self._out
         o.obs, o.reward, o.done, o.success, o.error = (p(self.obs), p(self.reward), p(self.done), p(self.success),
                                                         p(self.error))
@@ -172,7 +201,16 @@ class CtrReachVecEnv(object):
         if seed is not None:
             self.seed_value = int(seed)
             self.cfg.seed = self.seed_value & 0xFFFFFFFFFFFFFFFF
+            if self.pool_depth:
+                self.pool_r.zero_()          # precomputed resets belong to the old seed
         return [self.seed_value]
+
+    def refill_pool(self, stream=None):
+        """Precompute the queued resets into the pool (ctr_pool_refill); asynchronous."""
+        if self.pool_depth:
+            rc = self.lib.ctr_pool_refill(self.cfg, self._batch, _abi.stream_ptr(stream))
+            _abi.check(rc, "ctr_pool_refill")
+        self._steps_since_refill = 0
 
     def reset(self, goal=None, system=None, mask=None, stream=None):
         """CtrReachEnv.reset for all envs (or those with mask != 0).  goal: [N,3] f64 tensor or
@@ -194,6 +232,7 @@ class CtrReachVecEnv(object):
         rc = self.lib.ctr_reset(self.cfg, self._batch, _abi.ptr(m), _abi.ptr(g), _abi.ptr(s), _abi.ptr(self.obs),
                                 _abi.ptr(self.status), _abi.stream_ptr(stream))
         _abi.check(rc, "ctr_reset")
+        self.refill_pool(stream)
         return self._obs_dict()
 
     def step(self, actions, stream=None):
@@ -207,9 +246,7 @@ class CtrReachVecEnv(object):
             raise ValueError("actions must be [%d, 6]" % self.num_envs)
         self.cfg.tol = float(self.goal_tolerance.get_tol())
         self._last_actions = actions
-        rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
-                               _abi.stream_ptr(stream))
-        _abi.check(rc, "ctr_step")
+        self.step_raw(actions, stream)
         info = {"is_success": self.success.bool(), "error": self.error,
                 "terminal_observation": self.terminal_obs, "terminal_achieved_goal": self.terminal_achieved,
                 "status": self.status}
@@ -221,6 +258,10 @@ class CtrReachVecEnv(object):
                                _abi.stream_ptr(stream))
         if rc:
             _abi.check(rc, "ctr_step")
+        if self.pool_depth:
+            self._steps_since_refill += 1
+            if self._steps_since_refill >= self.refill_interval:
+                self.refill_pool(stream)
 
     def compute_reward(self, achieved_goal, desired_goal, info=None):
         """compute_reward (ctr_reach_env.py:160-170), batched over leading dims.  Device tensors

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 1
+#define CTR_ABI_VERSION 2
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -89,6 +89,22 @@ typedef struct ctr_batch_t {
     float    *starting_joints;   /* [n][6] or NULL (info q_starting)                  */
     double   *starting_position; /* [n][3] or NULL                                    */
     int32_t  *work;              /* [n+1] scratch for the auto-reset list (device)    */
+    /* Reset pool (optional, pool_depth 0 disables it).  Resets are a deterministic function of
+     * (seed, global env id, reset number), so they can be computed ahead of time: slot (r mod P)
+     * of env e holds reset number r (pool_r), precomputed by ctr_pool_refill; an auto-reset
+     * consumes it with a copy instead of two forward-kinematics solves.  A missing slot falls
+     * back to computing the reset in the same ctr_step call.  Layout [P][n][k]. */
+    int32_t   pool_depth;        /* P (0 = no pool)                                   */
+    int32_t   pool_pad;
+    float    *pool_qd;           /* [P][n][6] desired joints                          */
+    double   *pool_dg;           /* [P][n][3] desired goal                            */
+    float    *pool_q0;           /* [P][n][6] start joints                            */
+    double   *pool_ag;           /* [P][n][3] start position                          */
+    int32_t  *pool_sys;          /* [P][n]    system index                            */
+    uint32_t *pool_r;            /* [P][n]    reset number held (0 = empty)           */
+    uint32_t *pool_stat;         /* [P][n]    CTR_STATUS_* of the precomputation      */
+    int32_t  *refill;            /* [1 + 2 refill_cap]: count, then (env, reset number) */
+    int64_t   refill_cap;
 } ctr_batch_t;
 
 /* Per-step outputs (device). obs_dim = 13, or 14 when n_systems > 1 (obs.py:153-156). */
@@ -128,6 +144,11 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
  * Writes the reset observation to obs [n][obs_dim]. */
 int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8_t *mask,
               const double *goal, const int32_t *system, float *obs, uint32_t *status, void *stream);
+
+/* Precompute the resets queued in batch->refill (queued by ctr_step when a pooled reset is
+ * consumed, and by ctr_reset for the P resets after the one it computes), then clear the
+ * queue.  Call it every few steps; it is a no-op when the queue is empty. */
+int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
 
 /* Batched compute_reward over leading dims: ag, dg [n][3] f64 -> reward [n] f32 in {-1, 0}. */
 int ctr_compute_reward(const double *achieved, const double *desired, int64_t n, double tol,

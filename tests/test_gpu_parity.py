@@ -241,3 +241,26 @@ def test_facade_gym_surface(cuda):
     assert r == reward
     with pytest.raises(SystemExit):
         env.close()
+
+
+@pytest.mark.parametrize("depth,interval", [(4, 8), (1, 1000), (2, 3)])
+def test_reset_pool_matches_synchronous_resets(cuda, depth, interval):
+    """Pooled auto-resets (precomputed ahead of time, consumed by a copy; including pool misses
+    that fall back to the synchronous path) give bit-identical trajectories to computing every
+    reset at the step that needs it: a reset is a pure function of (seed, env id, reset number)."""
+    import torch
+    n = 4096
+    kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3])
+    a = _env(cuda, n, pool_depth=0, **kw)
+    b = _env(cuda, n, pool_depth=depth, refill_interval=interval, **kw)
+    a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03   # plenty of early successes
+    a.reset(); b.reset()
+    rng = np.random.default_rng(4)
+    for _ in range(13):
+        act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * a.action_space.high).astype(np.float32), device=cuda)
+        oa, ra, da, ia = a.step(act)
+        ob, rb, db, ib = b.step(act)
+        torch.cuda.synchronize()
+        for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs", "terminal_obs"):
+            np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(), err_msg=k)
+    assert (a.epoch.cpu().numpy() >= 4).all()
