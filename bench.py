@@ -152,16 +152,18 @@ def main():
     # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset
     j_probe = env.joints.clone()
     flops_env_step, sincos, nfev_mean = fk_work(env, j_probe)
-    env.autoreset = False
+    # ctr_step with autoreset = 0 launches exactly one kernel (k_step) on `stream`
+    from ctr_reach_amd import _abi
     k_iters = max(5, min(args.steps, 20))
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k_iters)]
+    sp = _abi.stream_ptr(stream)
     for i in range(k_iters):
         ev[i][0].record(stream)
-        env.step_raw(acts[i % len(acts)])
+        rc = env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[i % len(acts)]), env._out, 0, sp)
         ev[i][1].record(stream)
+        _abi.check(rc, "ctr_step")
     torch.cuda.synchronize()
     k_ms = sum(a.elapsed_time(b) for a, b in ev) / k_iters
-    env.autoreset = True
 
     if rank != 0:
         if dist:

@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "ctr_device.hpp"
 #include "ctr_reach_amd.h"
 
@@ -69,23 +71,28 @@ __device__ __forceinline__ void fk_dispatch(const ctr_system_t &sy, const float 
     fk_lane<HAS_UY>(sy, q, tip, st);
 }
 
-// Wave-aggregated append of `n_items` int32 per active lane to list (count at list[0]).
-__device__ __forceinline__ void wave_append(int32_t *list, int64_t cap, bool active, const int32_t *items,
-                                            int n_items)
+// Wave-aggregated append of `n_items` int32 per active lane to a list (one atomic per wave).
+__device__ __forceinline__ void wave_append(int32_t *counter, int32_t *items_base, int64_t cap, bool active,
+                                            const int32_t *items, int n_items)
 {
     const uint64_t m = __ballot(active);
     if (!m) return;
     const int lane = threadIdx.x & 63;
     const int leader = __builtin_ctzll(m);
     int base = 0;
-    if (lane == leader) base = atomicAdd(&list[0], __popcll(m));
+    if (lane == leader) base = atomicAdd(counter, __popcll(m));
     base = __shfl(base, leader);
     if (active) {
         const int64_t slot = base + __popcll(m & ((1ull << lane) - 1ull));
         if (slot < cap)
-            for (int k = 0; k < n_items; ++k) list[1 + n_items * slot + k] = items[k];
+            for (int k = 0; k < n_items; ++k) items_base[n_items * slot + k] = items[k];
     }
 }
+
+// Auto-reset miss list: counters work[0] / work[1] alternate between steps (work_parity) so the
+// consumer of one step's list can zero the next step's counter without a separate launch.
+__device__ __forceinline__ int32_t *miss_counter(const ctr_batch_t &b) { return b.work + (b.work_parity & 1); }
+__device__ __forceinline__ int32_t *miss_items(const ctr_batch_t &b) { return b.work + 2; }
 
 __device__ __forceinline__ void write_obs(float *dst, const float ob[14], bool multi)
 {
@@ -229,10 +236,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
     }
     if (autoreset) {
         const int32_t one[1] = {(int32_t)e};
-        wave_append(b.work, b.n, miss, one, 1);
+        wave_append(miss_counter(b), miss_items(b), b.n, miss, one, 1);
         if (b.pool_depth > 0) {
             const int32_t two[2] = {(int32_t)e, (int32_t)(pooled_r + (uint32_t)b.pool_depth)};
-            wave_append(b.refill, b.refill_cap, pooled, two, 2);
+            wave_append(b.refill, b.refill + 1, b.refill_cap, pooled, two, 2);
         }
     }
 }
@@ -296,7 +303,8 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const ctr_system_
     return ro;
 }
 
-// Synchronous reset.  mode 0: envs queued in b.work by k_step (pool misses / no pool);
+// Synchronous reset.  mode 0: envs queued in b.work by k_step (pool misses / no pool), swept
+// grid-stride by a small grid; it also zeroes the miss counter of the next step.
 // mode 1: all envs (or mask).  The pair's odd lane writes the env.
 template <bool HAS_UY>
 __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mode, const uint8_t *__restrict__ mask,
@@ -306,14 +314,18 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
 {
     __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
     __shared__ int s_count;
-    if (threadIdx.x == 0) s_count = (mode == 0) ? b.work[0] : 0;
+    if (threadIdx.x == 0) {
+        s_count = (mode == 0) ? min(*miss_counter(b), (int32_t)b.n) : 0;
+        if (mode == 0 && blockIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;   // next step's counter
+    }
     stage_systems(kc, s_sys);
-    if (mode == 0 && (int64_t)blockIdx.x * (BLOCK / 2) >= s_count) return;      // whole block idle
-    const int64_t slot = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 1;
+    const int64_t stride = (mode == 0) ? (int64_t)gridDim.x * (BLOCK / 2) : (int64_t)1 << 62;
+    for (int64_t base = (int64_t)blockIdx.x * (BLOCK / 2); mode != 0 || base < s_count; base += stride) {
+    const int64_t slot = base + (threadIdx.x >> 1);
     const bool odd = threadIdx.x & 1;
     int64_t e = -1;
     if (mode == 0) {
-        if (slot < s_count) e = b.work[1 + slot];
+        if (slot < s_count) e = miss_items(b)[slot];
     } else if (slot < b.n && (!mask || mask[slot])) {
         e = slot;
     }
@@ -356,15 +368,17 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
         // (re)queues r+1 .. r+P, skipping slots already holding the right reset
         if (mode == 0) {
             const int32_t two[2] = {(int32_t)ee, (int32_t)(r + (uint32_t)b.pool_depth)};
-            wave_append(b.refill, b.refill_cap, queue, two, 2);
+            wave_append(b.refill, b.refill + 1, b.refill_cap, queue, two, 2);
         } else {
             for (int j = 1; j <= b.pool_depth; ++j) {
                 const uint32_t rr = r + (uint32_t)j;
                 const bool need = queue && b.pool_r[(int64_t)(rr % (uint32_t)b.pool_depth) * b.n + ee] != rr;
                 const int32_t two[2] = {(int32_t)ee, (int32_t)rr};
-                wave_append(b.refill, b.refill_cap, need, two, 2);
+                wave_append(b.refill, b.refill + 1, b.refill_cap, need, two, 2);
             }
         }
+    }
+    if (mode != 0) break;
     }
 }
 
@@ -501,11 +515,12 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    if (autoreset) hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.work);
     launch2(kc.has_uy != 0, k_step<false>, k_step<true>, dim3(grid_for(b.n)), s, kc, b, actions, o, autoreset);
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset) {
-        launch2(kc.has_uy != 0, k_reset<false>, k_reset<true>, dim3(grid_for(2 * b.n)), s, kc, b, 0,
+        // misses are rare with a pool: a small grid sweeps the list grid-stride
+        const unsigned g = b.pool_depth > 0 ? std::min(grid_for(2 * b.n), 64u) : grid_for(2 * b.n);
+        launch2(kc.has_uy != 0, k_reset<false>, k_reset<true>, dim3(g), s, kc, b, 0,
                 (const uint8_t *)nullptr, (const double *)nullptr, (const int32_t *)nullptr, o.obs, o.status);
         return hip_check("ctr_step reset launch");
     }

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 2
+CTR_ABI_VERSION = 3
 CTR_MAX_SYSTEMS = 8
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1
@@ -56,6 +56,8 @@ class CtrBatch(ctypes.Structure):
         ("starting_joints", _P),
         ("starting_position", _P),
         ("work", _P),
+        ("work_parity", ctypes.c_int32),
+        ("work_pad", ctypes.c_int32),
         ("pool_depth", ctypes.c_int32),
         ("pool_pad", ctypes.c_int32),
         ("pool_qd", _P),

@@ -79,7 +79,7 @@ class CtrReachVecEnv(object):
     ``autoreset``.  Missing reference kwargs take the CTR-Reach-v0 registration defaults."""
 
     def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
-                 pool_depth=None, refill_interval=8, **kwargs):
+                 pool_depth=None, refill_interval=32, **kwargs):
         torch = _torch()
         kw = default_kwargs()
         kw.update(kwargs)
@@ -126,7 +126,7 @@ class CtrReachVecEnv(object):
         self.t = torch.zeros(n, dtype=i32, device=dev)
         self.system = torch.zeros(n, dtype=i32, device=dev)
         self.epoch = torch.zeros(n, dtype=i32, device=dev)
-        self.work = torch.zeros(n + 1, dtype=i32, device=dev)
+        self.work = torch.zeros(n + 2, dtype=i32, device=dev)
         self.desired_joints = torch.zeros((n, 6), dtype=f32, device=dev) if record_info else None
         self.starting_joints = torch.zeros((n, 6), dtype=f32, device=dev) if record_info else None
         self.starting_position = torch.zeros((n, 3), dtype=f64, device=dev) if record_info else None
@@ -143,7 +143,7 @@ class CtrReachVecEnv(object):
         # reset pool: resets are a pure function of (seed, env id, reset number), so they are
         # precomputed in batches every `refill_interval` steps and consumed by a copy
         if pool_depth is None:
-            pool_depth = 4 if (self.autoreset and self.resample_joints) else 0
+            pool_depth = 8 if (self.autoreset and self.resample_joints) else 0
         if pool_depth and not self.resample_joints:
             raise ValueError("the reset pool needs resample_joints=True")
         self.pool_depth = int(pool_depth)
@@ -258,6 +258,8 @@ class CtrReachVecEnv(object):
                                _abi.stream_ptr(stream))
         if rc:
             _abi.check(rc, "ctr_step")
+        if self.autoreset:
+            self._batch.work_parity ^= 1
         if self.pool_depth:
             self._steps_since_refill += 1
             if self._steps_since_refill >= self.refill_interval:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 2
+#define CTR_ABI_VERSION 3
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -88,7 +88,9 @@ typedef struct ctr_batch_t {
     float    *desired_joints;    /* [n][6] or NULL (info q_desired)                   */
     float    *starting_joints;   /* [n][6] or NULL (info q_starting)                  */
     double   *starting_position; /* [n][3] or NULL                                    */
-    int32_t  *work;              /* [n+1] scratch for the auto-reset list (device)    */
+    int32_t  *work;              /* [n+2] auto-reset miss list: 2 counters, then ids  */
+    int32_t   work_parity;       /* host toggles 0/1 every ctr_step: which counter   */
+    int32_t   work_pad;
     /* Reset pool (optional, pool_depth 0 disables it).  Resets are a deterministic function of
      * (seed, global env id, reset number), so they can be computed ahead of time: slot (r mod P)
      * of env e holds reset number r (pool_r), precomputed by ctr_pool_refill; an auto-reset
