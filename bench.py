@@ -115,10 +115,11 @@ def main():
     import torch
     dist, rank, ws, local = dist_init()
     from ctr_reach_amd import CtrReachVecEnv
+    from ctr_reach_amd import distributed as D
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     n = args.envs
-    env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=rank * n, autoreset=True, record_info=False)
+    env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False)
     env.reset()
     acts = make_actions(env, 8, args.seed + rank)
     stream = torch.cuda.current_stream()
@@ -142,11 +143,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    el = time.perf_counter() - t0
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = el_t.item()
+    el = D.max_over_ranks(time.perf_counter() - t0, device=dev)
     total_steps = n * ws * args.steps
 
     # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset

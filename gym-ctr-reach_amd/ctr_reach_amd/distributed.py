@@ -1,0 +1,63 @@
+"""Multi-GPU helpers: one process per GPU, environments sharded by global id.
+
+Environments are independent, so the step itself has no exchange: rank r owns the contiguous
+global ids [r * n, (r + 1) * n) (``env_base``) and every random draw is keyed by the global id,
+which makes results independent of the number of GPUs.  The only collective is OPTIONAL and off
+the data path: ``all_gather_outputs`` packs (tip x/y/z, reward, done | success << 1) into 20 B per
+env and all-gathers it over RCCL (backend "nccl" on ROCm, xGMI between the GPUs of a node) for a
+single-process trainer that wants every shard's outputs.
+"""
+import os
+
+PACK_WIDTH = 5   # float32 words per env: tip x, y, z, reward, flags (done | success << 1)
+
+
+def world():
+    """(rank, world_size, local_rank) from the torchrun environment (1 process if unset)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard(num_envs_per_rank, rank):
+    """Global id of this rank's first environment."""
+    return int(num_envs_per_rank) * int(rank)
+
+
+def pack_step_outputs(achieved_goal, reward, done, success, out=None):
+    """[n, 5] float32 tensor: tip (3, f64 -> f32), reward, done | success << 1."""
+    import torch
+    n = achieved_goal.shape[0]
+    if out is None:
+        out = torch.empty((n, PACK_WIDTH), dtype=torch.float32, device=achieved_goal.device)
+    out[:, 0:3] = achieved_goal
+    out[:, 3] = reward
+    out[:, 4] = done.to(torch.float32) + 2.0 * success.to(torch.float32)
+    return out
+
+
+def unpack_step_outputs(packed):
+    import torch
+    flags = packed[:, 4].round().to(torch.int32)
+    return packed[:, 0:3], packed[:, 3], (flags & 1).bool(), (flags & 2).bool()
+
+
+def all_gather_outputs(packed, group=None):
+    """All-gather every rank's packed [n, 5] block into [world * n, 5] (rank-major = global id
+    order).  Uses all_gather_into_tensor: one RCCL ring/tree call for the whole step."""
+    import torch
+    import torch.distributed as dist
+    ws = dist.get_world_size(group)
+    out = torch.empty((ws * packed.shape[0], packed.shape[1]), dtype=packed.dtype, device=packed.device)
+    dist.all_gather_into_tensor(out, packed.contiguous(), group=group)
+    return out
+
+
+def max_over_ranks(value, device=None, group=None):
+    """Max of a python float over ranks (bench timing); identity without a process group."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

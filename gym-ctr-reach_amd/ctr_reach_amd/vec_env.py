@@ -302,6 +302,17 @@ class CtrReachVecEnv(object):
             return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=stats[:, 2], nseg=stats[:, 3], status=status)
         return tip
 
+    def gather_outputs(self, group=None):
+        """Optional collective for a single-process trainer: every rank's last-step (tip, reward,
+        done, success) packed to 20 B/env and all-gathered over RCCL -> [world * n, 5] float32
+        in global-id order.  Not used on the stepping path."""
+        import torch
+        from . import distributed as D
+        d = self.done.bool()
+        tip = torch.where(d[:, None], self.terminal_achieved, self.achieved_goal) if self.autoreset else self.achieved_goal
+        self._packed = D.pack_step_outputs(tip, self.reward, d, self.success, out=getattr(self, "_packed", None))
+        return D.all_gather_outputs(self._packed, group=group)
+
     def update_goal_tolerance(self, timestep):
         self.goal_tolerance.update(timestep)
 
