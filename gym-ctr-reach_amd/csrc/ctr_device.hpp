@@ -21,6 +21,7 @@
 namespace ctr {
 
 constexpr int NS = 18;  // [u_z(3), alpha(3), r(3), R row-major(9)]   (model.py:136)
+constexpr int CTR_BLOCK = 256;   // every kernel runs 256-lane workgroups (per-lane LDS slots below)
 
 // ------------------------------------------------------------------------------------------
 // Segmentation (Segment.py:6-61).  Ten transition points [0, beta, d_c, d_tip] are sorted,
@@ -28,8 +29,9 @@ constexpr int NS = 18;  // [u_z(3), alpha(3), r(3), R row-major(9)]   (model.py:
 // kept "raw" (9 gaps in sorted order, many of which are dropped later) so that every array
 // index is static; integration walks the gaps with a cursor.
 // ------------------------------------------------------------------------------------------
+// The 9 gap end points (cumsum(len[0..k]) + min(beta)) live in LDS, one column per lane
+// (s_end[k][lane]: conflict-free, dynamically indexable, off the VGPR budget).
 struct Seg {
-    double end[9];     // cumsum(len[0..k]) + min(beta): end arclength of raw gap k
     uint32_t kept;     // bit k: gap k has non-zero length and ends after s = 0 (kept in S)
     uint64_t mask;     // 6 bits per gap: bits 0-2 tube i present (EI != 0), 3-5 tube i curved
 };
@@ -43,7 +45,7 @@ __device__ __forceinline__ void cswap(double &a, double &b, int &ia, int &ib)
     a = ta; b = tb; ia = ja; ib = jb;
 }
 
-__device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double beta[3])
+__device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double beta[3], double *end_lds)
 {
 #pragma clang fp contract(off)
     double v[10];
@@ -104,7 +106,7 @@ __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double be
     #pragma unroll
     for (int k = 0; k < 9; ++k) {         // :46-55 (adding a zero gap is an exact no-op)
         cum += len[k];
-        sg.end[k] = cum + bmin;
+        end_lds[k * CTR_BLOCK] = cum + bmin;
         sg.kept |= ((len[k] != 0.0) && (cum + bmin > 0.0)) ? (1u << k) : 0u;
     }
     return sg;
@@ -164,8 +166,15 @@ struct Trig {
 __device__ __forceinline__ Trig trig_of(const double al[3])
 {
     Trig t;
-    ctr_math::sincos_cw(al[1] - al[0], &t.s10, &t.c10);
-    ctr_math::sincos_cw(al[2] - al[0], &t.s20, &t.c20);
+    const double d10 = al[1] - al[0], d20 = al[2] - al[0];
+    // both reductions branch-free and interleavable; the exact slow path only when some lane
+    // of the wave has a huge / non-finite angle (wave-uniform branch)
+    ctr_math::sincos_fast(d10, t.s10, t.c10);
+    ctr_math::sincos_fast(d20, t.s20, t.c20);
+    if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10) || ctr_math::sincos_needs_slow(d20)) != 0, 0)) {
+        if (ctr_math::sincos_needs_slow(d10)) ctr_math::sincos_slow(d10, &t.s10, &t.c10);
+        if (ctr_math::sincos_needs_slow(d20)) ctr_math::sincos_slow(d20, &t.s20, &t.c20);
+    }
     // alpha_2 - alpha_1 = (alpha_2 - alpha_0) - (alpha_1 - alpha_0): angle-difference identity
     t.c21 = t.c20 * t.c10 + t.s20 * t.s10;
     t.s21 = t.s20 * t.c10 - t.c20 * t.s10;
@@ -251,7 +260,9 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
 {
     using namespace rk;
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};
-    const Seg sg = seg_build(sy, beta);
+    __shared__ double s_end[9][CTR_BLOCK];
+    double *end_lds = &s_end[0][threadIdx.x];
+    const Seg sg = seg_build(sy, beta, end_lds);
 
     // state y = [u_z(3), alpha(3), r(3), R(9)]
     double yu[3] = {0.0, 0.0, 0.0};
@@ -273,12 +284,18 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
     bool need_init = true, new_step = true, rejected = false;
 
     for (;;) {
+#ifdef CTR_DIAG_WAVE
+        // diagnostic build: wave-uniform counts of loop iterations / iterations running the
+        // segment-start block (reported in place of nrej / nseg)
+        st.nrej++;
+        if (__ballot(need_init && remaining != 0)) st.nseg++;
+#endif
         if (need_init) {
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
             p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u));
-            const double endk = sel9(sg.end, k);
+            const double endk = end_lds[k * CTR_BLOCK];
             const double a = prev_end, b = endk - 1e-6;          // model.py:141 linspace endpoints
             const double t0 = fmin(a, b);
             tb = fmax(a, b);                                      // :145-151 sorted span
@@ -288,7 +305,9 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             double fr[3];
             stage_at(p, ty, yu, yR, f, fr);
             st.nfev++;
+#ifndef CTR_DIAG_WAVE
             st.nseg++;
+#endif
             const double interval = tb - t0;
             if (interval == 0.0) continue;                        // OdeSolver.step: t == t_bound
             // select_initial_step (common.py:68-140), order 4, direction +1
@@ -427,20 +446,21 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
         rhs_core<HAS_UY>(p, tn, nu, nR, K6.uz, K6.R);
         stage_at(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
-        // error norm: RMS of h * (K^T E) / (atol + max(|y|, |y_new|) rtol)
+        // error norm: RMS of h * (K^T E) / (atol + max(|y|, |y_new|) rtol); |h| factored out
         double en2 = 0.0;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double xu = ((eu[i] + K6.uz[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(yu[i]), fabs(nu[i])) * RTOL);
-            const double xa = ((ea[i] + K6.al[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(ya[i]), fabs(na[i])) * RTOL);
-            const double xr = ((er[i] + k6r[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(yr[i]), fabs(nr[i])) * RTOL);
-            en2 += xu * xu + xa * xa + xr * xr;
+            const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp1(fma(fmax(fabs(yu[i]), fabs(nu[i])), RTOL, ATOL));
+            const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp1(fma(fmax(fabs(ya[i]), fabs(na[i])), RTOL, ATOL));
+            const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp1(fma(fmax(fabs(yr[i]), fabs(nr[i])), RTOL, ATOL));
+            en2 = fma(xu, xu, fma(xa, xa, fma(xr, xr, en2)));
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const double xR = ((eR[i] + K6.R[i] * E6) * h) * ctr_math::rcp(ATOL + fmax(fabs(yR[i]), fabs(nR[i])) * RTOL);
-            en2 += xR * xR;
+            const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp1(fma(fmax(fabs(yR[i]), fabs(nR[i])), RTOL, ATOL));
+            en2 = fma(xR, xR, en2);
         }
+        en2 *= h * h;
         const double en = sqrt(en2) * INV_SQRT18;
         if (en < 1.0) {
             double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * ctr_math::powpos(en, -0.2));
@@ -459,7 +479,9 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
         } else {
             ha *= fmax(0.2, 0.9 * ctr_math::powpos(en, -0.2));
             rejected = true;
+#ifndef CTR_DIAG_WAVE
             st.nrej++;
+#endif
         }
     }
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];

@@ -28,12 +28,9 @@ void sincos_slow(double x, double *sp, double *cp)
     *cp = cos(x);
 }
 
-CTR_HD void sincos_cw(double x, double *sp, double *cp)
+// Fast path only (valid for |x| < 2^20): Cody-Waite + minimax kernels, branch-free.
+CTR_HD void sincos_fast(double x, double &sv, double &cv)
 {
-    if (!(fabs(x) < 1048576.0)) {                 // rare: huge or non-finite arguments
-        sincos_slow(x, sp, cp);
-        return;
-    }
     const double n = rint(x * 0.6366197723675814);             // round(x * 2/pi)
     double r = fma(-n, 1.5707963267948966, x);                 // pi/2 = P1 + P2 + P3
     r = fma(-n, 6.123233995736766e-17, r);
@@ -57,8 +54,19 @@ CTR_HD void sincos_cw(double x, double *sp, double *cp)
     const int q = ((int)n) & 3;
     const double ss = (q & 1) ? c : s;
     const double cc = (q & 1) ? s : c;
-    *sp = (q & 2) ? -ss : ss;
-    *cp = ((q + 1) & 2) ? -cc : cc;
+    sv = (q & 2) ? -ss : ss;
+    cv = ((q + 1) & 2) ? -cc : cc;
+}
+
+CTR_HD bool sincos_needs_slow(double x) { return !(fabs(x) < 1048576.0); }
+
+CTR_HD void sincos_cw(double x, double *sp, double *cp)
+{
+    if (sincos_needs_slow(x)) {                   // rare: huge or non-finite arguments
+        sincos_slow(x, sp, cp);
+        return;
+    }
+    sincos_fast(x, *sp, *cp);
 }
 
 // 1/x to within 1 ulp: hardware reciprocal estimate + two Newton-Raphson steps.
@@ -70,6 +78,17 @@ CTR_HD double rcp(double x)
     r = fma(r, e, r);
     e = fma(-x, r, 1.0);
     return fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+
+// 1/x to about 1 ulp with a single Newton-Raphson step (step-size control only).
+CTR_HD double rcp1(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double r = __builtin_amdgcn_rcp(x);
+    return fma(r, fma(-x, r, 1.0), r);
 #else
     return 1.0 / x;
 #endif
