@@ -314,12 +314,12 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             double isc_u[3], isc_a[3], isc_r[3], isc_R[9];
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                isc_u[i] = ctr_math::rcp(ATOL + fabs(yu[i]) * RTOL);
-                isc_a[i] = ctr_math::rcp(ATOL + fabs(ya[i]) * RTOL);
-                isc_r[i] = ctr_math::rcp(ATOL + fabs(yr[i]) * RTOL);
+                isc_u[i] = ctr_math::rcp1(ATOL + fabs(yu[i]) * RTOL);
+                isc_a[i] = ctr_math::rcp1(ATOL + fabs(ya[i]) * RTOL);
+                isc_r[i] = ctr_math::rcp1(ATOL + fabs(yr[i]) * RTOL);
             }
             #pragma unroll
-            for (int i = 0; i < 9; ++i) isc_R[i] = ctr_math::rcp(ATOL + fabs(yR[i]) * RTOL);
+            for (int i = 0; i < 9; ++i) isc_R[i] = ctr_math::rcp1(ATOL + fabs(yR[i]) * RTOL);
             double s0 = 0.0, s1 = 0.0;
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -396,13 +396,19 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
 
         Stage K1, K2, K3, K4, K5;
         double ui[3], ai[3], Ri[9], rc[3];
+        // stage coefficients pre-multiplied by h: y + sum_j K_j (a_sj h)
+        const double a10 = A10 * h;
+        const double a20 = A20 * h, a21 = A21 * h;
+        const double a30 = A30 * h, a31 = A31 * h, a32 = A32 * h;
+        const double a40 = A40 * h, a41 = A41 * h, a42 = A42 * h, a43 = A43 * h;
+        const double a50 = A50 * h, a51 = A51 * h, a52 = A52 * h, a53 = A53 * h, a54 = A54 * h;
 #define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF)                                  \
         {                                                                                      \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
-                ui[i] = yu[i] + (EXPR_U) * h;                                                  \
-                ai[i] = ya[i] + (EXPR_A) * h;                                                  \
+                ui[i] = yu[i] + (EXPR_U);                                                      \
+                ai[i] = ya[i] + (EXPR_A);                                                      \
             }                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = yR[i] + (EXPR_R) * h;        \
+            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = yR[i] + (EXPR_R);            \
             const Trig tt = trig_of(ai);                                                       \
             rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
             stage_at(p, tt, ui, Ri, KOUT, rc);                                                 \
@@ -411,33 +417,34 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
                 er[i] += rc[i] * (ECOEF);                                                      \
             }                                                                                  \
         }
-        CTR_STAGE(K1, f.uz[i] * A10, f.al[i] * A10, f.R[i] * A10, 0.0, 0.0)
-        CTR_STAGE(K2, f.uz[i] * A20 + K1.uz[i] * A21, f.al[i] * A20 + K1.al[i] * A21,
-                  f.R[i] * A20 + K1.R[i] * A21, B2, E2)
-        CTR_STAGE(K3, f.uz[i] * A30 + K1.uz[i] * A31 + K2.uz[i] * A32,
-                  f.al[i] * A30 + K1.al[i] * A31 + K2.al[i] * A32,
-                  f.R[i] * A30 + K1.R[i] * A31 + K2.R[i] * A32, B3, E3)
-        CTR_STAGE(K4, f.uz[i] * A40 + K1.uz[i] * A41 + K2.uz[i] * A42 + K3.uz[i] * A43,
-                  f.al[i] * A40 + K1.al[i] * A41 + K2.al[i] * A42 + K3.al[i] * A43,
-                  f.R[i] * A40 + K1.R[i] * A41 + K2.R[i] * A42 + K3.R[i] * A43, B4, E4)
-        CTR_STAGE(K5, f.uz[i] * A50 + K1.uz[i] * A51 + K2.uz[i] * A52 + K3.uz[i] * A53 + K4.uz[i] * A54,
-                  f.al[i] * A50 + K1.al[i] * A51 + K2.al[i] * A52 + K3.al[i] * A53 + K4.al[i] * A54,
-                  f.R[i] * A50 + K1.R[i] * A51 + K2.R[i] * A52 + K3.R[i] * A53 + K4.R[i] * A54, B5, E5)
+        CTR_STAGE(K1, f.uz[i] * a10, f.al[i] * a10, f.R[i] * a10, 0.0, 0.0)
+        CTR_STAGE(K2, f.uz[i] * a20 + K1.uz[i] * a21, f.al[i] * a20 + K1.al[i] * a21,
+                  f.R[i] * a20 + K1.R[i] * a21, B2, E2)
+        CTR_STAGE(K3, f.uz[i] * a30 + K1.uz[i] * a31 + K2.uz[i] * a32,
+                  f.al[i] * a30 + K1.al[i] * a31 + K2.al[i] * a32,
+                  f.R[i] * a30 + K1.R[i] * a31 + K2.R[i] * a32, B3, E3)
+        CTR_STAGE(K4, f.uz[i] * a40 + K1.uz[i] * a41 + K2.uz[i] * a42 + K3.uz[i] * a43,
+                  f.al[i] * a40 + K1.al[i] * a41 + K2.al[i] * a42 + K3.al[i] * a43,
+                  f.R[i] * a40 + K1.R[i] * a41 + K2.R[i] * a42 + K3.R[i] * a43, B4, E4)
+        CTR_STAGE(K5, f.uz[i] * a50 + K1.uz[i] * a51 + K2.uz[i] * a52 + K3.uz[i] * a53 + K4.uz[i] * a54,
+                  f.al[i] * a50 + K1.al[i] * a51 + K2.al[i] * a52 + K3.al[i] * a53 + K4.al[i] * a54,
+                  f.R[i] * a50 + K1.R[i] * a51 + K2.R[i] * a52 + K3.R[i] * a53 + K4.R[i] * a54, B5, E5)
 #undef CTR_STAGE
         // y_new (rk.py rk_step) and the error sums without K6
         double nu[3], na[3], nr[3], nR[9];
         double eu[3], ea[3], eR[9];
+        const double b0 = B0 * h, b2 = B2 * h, b3 = B3 * h, b4 = B4 * h, b5 = B5 * h;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            nu[i] = yu[i] + h * (f.uz[i] * B0 + K2.uz[i] * B2 + K3.uz[i] * B3 + K4.uz[i] * B4 + K5.uz[i] * B5);
-            na[i] = ya[i] + h * (f.al[i] * B0 + K2.al[i] * B2 + K3.al[i] * B3 + K4.al[i] * B4 + K5.al[i] * B5);
+            nu[i] = yu[i] + (f.uz[i] * b0 + K2.uz[i] * b2 + K3.uz[i] * b3 + K4.uz[i] * b4 + K5.uz[i] * b5);
+            na[i] = ya[i] + (f.al[i] * b0 + K2.al[i] * b2 + K3.al[i] * b3 + K4.al[i] * b4 + K5.al[i] * b5);
             nr[i] = yr[i] + h * br[i];
             eu[i] = f.uz[i] * E0 + K2.uz[i] * E2 + K3.uz[i] * E3 + K4.uz[i] * E4 + K5.uz[i] * E5;
             ea[i] = f.al[i] * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5;
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            nR[i] = yR[i] + h * (f.R[i] * B0 + K2.R[i] * B2 + K3.R[i] * B3 + K4.R[i] * B4 + K5.R[i] * B5);
+            nR[i] = yR[i] + (f.R[i] * b0 + K2.R[i] * b2 + K3.R[i] * b3 + K4.R[i] * b4 + K5.R[i] * b5);
             eR[i] = f.R[i] * E0 + K2.R[i] * E2 + K3.R[i] * E3 + K4.R[i] * E4 + K5.R[i] * E5;
         }
         Stage K6;
