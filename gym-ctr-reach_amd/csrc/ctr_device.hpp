@@ -172,8 +172,16 @@ __device__ __forceinline__ Trig trig_of(const double al[3])
     ctr_math::sincos_fast(d10, t.s10, t.c10);
     ctr_math::sincos_fast(d20, t.s20, t.c20);
     if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10) || ctr_math::sincos_needs_slow(d20)) != 0, 0)) {
-        if (ctr_math::sincos_needs_slow(d10)) ctr_math::sincos_slow(d10, &t.s10, &t.c10);
-        if (ctr_math::sincos_needs_slow(d20)) ctr_math::sincos_slow(d20, &t.s20, &t.c20);
+        if (ctr_math::sincos_needs_slow(d10)) {
+            const ctr_math::SinCos r = ctr_math::sincos_slow(d10);
+            t.s10 = r.s;
+            t.c10 = r.c;
+        }
+        if (ctr_math::sincos_needs_slow(d20)) {
+            const ctr_math::SinCos r = ctr_math::sincos_slow(d20);
+            t.s20 = r.s;
+            t.c20 = r.c;
+        }
     }
     // alpha_2 - alpha_1 = (alpha_2 - alpha_0) - (alpha_1 - alpha_0): angle-difference identity
     t.c21 = t.c20 * t.c10 + t.s20 * t.s10;

@@ -15,17 +15,23 @@
 
 namespace ctr_math {
 
+struct SinCos {
+    double s, c;
+};
+
 // Out-of-line slow path (keeps the math library's large-argument reduction out of every
-// inlined call site).
+// inlined call site).  Returns by value so callers keep their operands in registers.
 #if defined(__HIPCC__)
 __host__ __device__ __attribute__((noinline))
 #else
 static
 #endif
-void sincos_slow(double x, double *sp, double *cp)
+SinCos sincos_slow(double x)
 {
-    *sp = sin(x);
-    *cp = cos(x);
+    SinCos r;
+    r.s = sin(x);
+    r.c = cos(x);
+    return r;
 }
 
 // Fast path only (valid for |x| < 2^20): Cody-Waite + minimax kernels, branch-free.
@@ -63,7 +69,9 @@ CTR_HD bool sincos_needs_slow(double x) { return !(fabs(x) < 1048576.0); }
 CTR_HD void sincos_cw(double x, double *sp, double *cp)
 {
     if (sincos_needs_slow(x)) {                   // rare: huge or non-finite arguments
-        sincos_slow(x, sp, cp);
+        const SinCos r = sincos_slow(x);
+        *sp = r.s;
+        *cp = r.c;
         return;
     }
     sincos_fast(x, *sp, *cp);
