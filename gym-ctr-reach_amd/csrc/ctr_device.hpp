@@ -413,10 +413,10 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
 #define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF)                                  \
         {                                                                                      \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
-                ui[i] = yu[i] + (EXPR_U);                                                      \
-                ai[i] = ya[i] + (EXPR_A);                                                      \
+                ui[i] = EXPR_U;                                                                \
+                ai[i] = EXPR_A;                                                                \
             }                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = yR[i] + (EXPR_R);            \
+            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = EXPR_R;                      \
             const Trig tt = trig_of(ai);                                                       \
             rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
             stage_at(p, tt, ui, Ri, KOUT, rc);                                                 \
@@ -425,18 +425,21 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
                 er[i] += rc[i] * (ECOEF);                                                      \
             }                                                                                  \
         }
-        CTR_STAGE(K1, f.uz[i] * a10, f.al[i] * a10, f.R[i] * a10, 0.0, 0.0)
-        CTR_STAGE(K2, f.uz[i] * a20 + K1.uz[i] * a21, f.al[i] * a20 + K1.al[i] * a21,
-                  f.R[i] * a20 + K1.R[i] * a21, B2, E2)
-        CTR_STAGE(K3, f.uz[i] * a30 + K1.uz[i] * a31 + K2.uz[i] * a32,
-                  f.al[i] * a30 + K1.al[i] * a31 + K2.al[i] * a32,
-                  f.R[i] * a30 + K1.R[i] * a31 + K2.R[i] * a32, B3, E3)
-        CTR_STAGE(K4, f.uz[i] * a40 + K1.uz[i] * a41 + K2.uz[i] * a42 + K3.uz[i] * a43,
-                  f.al[i] * a40 + K1.al[i] * a41 + K2.al[i] * a42 + K3.al[i] * a43,
-                  f.R[i] * a40 + K1.R[i] * a41 + K2.R[i] * a42 + K3.R[i] * a43, B4, E4)
-        CTR_STAGE(K5, f.uz[i] * a50 + K1.uz[i] * a51 + K2.uz[i] * a52 + K3.uz[i] * a53 + K4.uz[i] * a54,
-                  f.al[i] * a50 + K1.al[i] * a51 + K2.al[i] * a52 + K3.al[i] * a53 + K4.al[i] * a54,
-                  f.R[i] * a50 + K1.R[i] * a51 + K2.R[i] * a52 + K3.R[i] * a53 + K4.R[i] * a54, B5, E5)
+        CTR_STAGE(K1, fma(f.uz[i], a10, yu[i]),
+                  fma(f.al[i], a10, ya[i]),
+                  fma(f.R[i], a10, yR[i]), 0.0, 0.0)
+        CTR_STAGE(K2, fma(K1.uz[i], a21, fma(f.uz[i], a20, yu[i])),
+                  fma(K1.al[i], a21, fma(f.al[i], a20, ya[i])),
+                  fma(K1.R[i], a21, fma(f.R[i], a20, yR[i])), B2, E2)
+        CTR_STAGE(K3, fma(K2.uz[i], a32, fma(K1.uz[i], a31, fma(f.uz[i], a30, yu[i]))),
+                  fma(K2.al[i], a32, fma(K1.al[i], a31, fma(f.al[i], a30, ya[i]))),
+                  fma(K2.R[i], a32, fma(K1.R[i], a31, fma(f.R[i], a30, yR[i]))), B3, E3)
+        CTR_STAGE(K4, fma(K3.uz[i], a43, fma(K2.uz[i], a42, fma(K1.uz[i], a41, fma(f.uz[i], a40, yu[i])))),
+                  fma(K3.al[i], a43, fma(K2.al[i], a42, fma(K1.al[i], a41, fma(f.al[i], a40, ya[i])))),
+                  fma(K3.R[i], a43, fma(K2.R[i], a42, fma(K1.R[i], a41, fma(f.R[i], a40, yR[i])))), B4, E4)
+        CTR_STAGE(K5, fma(K4.uz[i], a54, fma(K3.uz[i], a53, fma(K2.uz[i], a52, fma(K1.uz[i], a51, fma(f.uz[i], a50, yu[i]))))),
+                  fma(K4.al[i], a54, fma(K3.al[i], a53, fma(K2.al[i], a52, fma(K1.al[i], a51, fma(f.al[i], a50, ya[i]))))),
+                  fma(K4.R[i], a54, fma(K3.R[i], a53, fma(K2.R[i], a52, fma(K1.R[i], a51, fma(f.R[i], a50, yR[i]))))), B5, E5)
 #undef CTR_STAGE
         // y_new (rk.py rk_step) and the error sums without K6
         double nu[3], na[3], nr[3], nR[9];
@@ -444,15 +447,15 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
         const double b0 = B0 * h, b2 = B2 * h, b3 = B3 * h, b4 = B4 * h, b5 = B5 * h;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            nu[i] = yu[i] + (f.uz[i] * b0 + K2.uz[i] * b2 + K3.uz[i] * b3 + K4.uz[i] * b4 + K5.uz[i] * b5);
-            na[i] = ya[i] + (f.al[i] * b0 + K2.al[i] * b2 + K3.al[i] * b3 + K4.al[i] * b4 + K5.al[i] * b5);
+            nu[i] = fma(K5.uz[i], b5, fma(K4.uz[i], b4, fma(K3.uz[i], b3, fma(K2.uz[i], b2, fma(f.uz[i], b0, yu[i])))));
+            na[i] = fma(K5.al[i], b5, fma(K4.al[i], b4, fma(K3.al[i], b3, fma(K2.al[i], b2, fma(f.al[i], b0, ya[i])))));
             nr[i] = yr[i] + h * br[i];
             eu[i] = f.uz[i] * E0 + K2.uz[i] * E2 + K3.uz[i] * E3 + K4.uz[i] * E4 + K5.uz[i] * E5;
             ea[i] = f.al[i] * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5;
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            nR[i] = yR[i] + (f.R[i] * b0 + K2.R[i] * b2 + K3.R[i] * b3 + K4.R[i] * b4 + K5.R[i] * b5);
+            nR[i] = fma(K5.R[i], b5, fma(K4.R[i], b4, fma(K3.R[i], b3, fma(K2.R[i], b2, fma(f.R[i], b0, yR[i])))));
             eR[i] = f.R[i] * E0 + K2.R[i] * E2 + K3.R[i] * E3 + K4.R[i] * E4 + K5.R[i] * E5;
         }
         Stage K6;

@@ -168,7 +168,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
         for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(sy, kc.c.constrain_alpha != 0, q, a);
         FkStats st = {0, 0, 0, 0, 0};
         double ag[3];
+#ifdef CTR_EXP_NOFK
+        ag[0] = q[0]; ag[1] = q[1]; ag[2] = q[2];      // experiment: step overhead without the FK
+#else
         fk_dispatch<HAS_UY>(sy, q, ag, st);
+#endif
         const int32_t t = b.t[e] + 1;
         double dg[3];
         #pragma unroll
