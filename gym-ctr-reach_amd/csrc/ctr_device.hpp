@@ -247,6 +247,20 @@ struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
 
+#ifdef CTR_DIAG_TIME
+__device__ __forceinline__ uint64_t stamp()
+{
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define CTR_STAMP(var) const uint64_t var = stamp()
+#else
+#define CTR_STAMP(var)
+#endif
+
 // Stage derivative storage: u_z' (3), alpha' (3), R' (9).  r' = column 3 of the stage input
 // R is folded straight into the B / E accumulators instead of being stored.
 struct Stage {
@@ -291,7 +305,12 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
     uint32_t remaining = sg.kept;   // kept gaps not yet integrated, in arclength order
     bool need_init = true, new_step = true, rejected = false;
 
+#ifdef CTR_DIAG_TIME
+    uint64_t c_init = 0, c_stage = 0, c_tail = 0;
+    CTR_STAMP(t_begin);
+#endif
     for (;;) {
+        CTR_STAMP(ts0);
 #ifdef CTR_DIAG_WAVE
         // diagnostic build: wave-uniform counts of loop iterations / iterations running the
         // segment-start block (reported in place of nrej / nseg)
@@ -341,8 +360,9 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
                 s0 += (yR[i] * isc_R[i]) * (yR[i] * isc_R[i]);
                 s1 += (f.R[i] * isc_R[i]) * (f.R[i] * isc_R[i]);
             }
-            const double d0 = sqrt(s0) * INV_SQRT18, d1 = sqrt(s1) * INV_SQRT18;
-            double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+            // d0 = ||y/sc||_rms, d1 = ||f/sc||_rms kept squared (no sqrt on the hot path)
+            const double d0sq = s0 * (1.0 / 18), d1sq = s1 * (1.0 / 18);
+            double h0 = (d0sq < 1e-10 || d1sq < 1e-10) ? 1e-6 : 0.01 * ctr_math::sqrt_rsq(s0 * ctr_math::rcp1(s1));
             h0 = fmin(h0, interval);
             double u1[3], a1[3], R1[9];
             #pragma unroll
@@ -369,16 +389,18 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
                 const double dR = (f1.R[i] - f.R[i]) * isc_R[i];
                 s2 += dR * dR;
             }
-            const double d2 = sqrt(s2) * INV_SQRT18 / h0;
+            const double ih0 = ctr_math::rcp1(h0);
+            const double d2sq = s2 * (1.0 / 18) * ih0 * ih0;            // d2^2
             double h1;
-            if (d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
-            else h1 = ctr_math::powpos(0.01 / fmax(d1, d2), 0.2);
+            if (d1sq <= 1e-30 && d2sq <= 1e-30) h1 = fmax(1e-6, h0 * 1e-3);
+            else h1 = 0.3981071705534972 * ctr_math::inv_root10(fmax(d1sq, d2sq));   // (0.01/max(d1,d2))^(1/5)
             ha = fmin(fmin(100.0 * h0, h1), interval);
             t = t0;
             need_init = false;
             new_step = true;
         }
 
+        CTR_STAMP(ts1);
         // ---- one attempt of RungeKutta._step_impl (rk.py:111-175) ----
         if (new_step) {
             min_step = 10.0 * fabs(nextafter(t, INFINITY) - t);
@@ -441,6 +463,7 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
                   fma(K4.al[i], a54, fma(K3.al[i], a53, fma(K2.al[i], a52, fma(K1.al[i], a51, fma(f.al[i], a50, ya[i]))))),
                   fma(K4.R[i], a54, fma(K3.R[i], a53, fma(K2.R[i], a52, fma(K1.R[i], a51, fma(f.R[i], a50, yR[i]))))), B5, E5)
 #undef CTR_STAGE
+        CTR_STAMP(ts2);
         // y_new (rk.py rk_step) and the error sums without K6
         double nu[3], na[3], nr[3], nR[9];
         double eu[3], ea[3], eR[9];
@@ -478,10 +501,18 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp1(fma(fmax(fabs(yR[i]), fabs(nR[i])), RTOL, ATOL));
             en2 = fma(xR, xR, en2);
         }
-        en2 *= h * h;
-        const double en = sqrt(en2) * INV_SQRT18;
-        if (en < 1.0) {
-            double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * ctr_math::powpos(en, -0.2));
+        en2 *= h * h;                       // = 18 error_norm^2
+        const double en2n = en2 * (1.0 / 18);   // error_norm^2
+        // error_norm ** -0.2 = (error_norm^2) ** -0.1
+        const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
+        CTR_STAMP(ts3);
+#ifdef CTR_DIAG_TIME
+        c_init += ts1 - ts0;
+        c_stage += ts2 - ts1;
+        c_tail += ts3 - ts2;
+#endif
+        if (en2n < 1.0) {
+            double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
             ha *= factor;
             #pragma unroll
@@ -495,13 +526,20 @@ __device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3],
             new_step = true;
             if (t - tb >= 0.0) need_init = true;    // segment finished (status 'finished')
         } else {
-            ha *= fmax(0.2, 0.9 * ctr_math::powpos(en, -0.2));
+            ha *= fmax(0.2, fpow);
             rejected = true;
 #ifndef CTR_DIAG_WAVE
             st.nrej++;
 #endif
         }
     }
+#ifdef CTR_DIAG_TIME
+    CTR_STAMP(t_end);
+    st.nfev = (uint32_t)c_init;
+    st.nstep = (uint32_t)c_stage;
+    st.nrej = (uint32_t)c_tail;
+    st.nseg = (uint32_t)(t_end - t_begin);
+#endif
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 }

@@ -102,6 +102,46 @@ CTR_HD double rcp1(double x)
 #endif
 }
 
+// x^(-1/10) for finite x > 0, ~1 ulp: x = x' 2^(10k) with x' in [1, 2^10); a float32
+// exp2/log2 seed for x'^(-1/10), two float64 Newton steps on y^10 x' = 1, then 2^(-k).
+// (Replaces pow(), ~5x cheaper; used by the RK45 step-size controller only.)
+CTR_HD double inv_root10(double x)
+{
+    int e;
+    const double m = frexp(x, &e);                       // x = m 2^e, m in [0.5, 1)
+    // write e - 1 = 10 k + r with r in [0, 10)
+    const int em1 = e - 1;
+    const int k = (em1 >= 0) ? em1 / 10 : -((9 - em1) / 10);
+    const int r = em1 - 10 * k;
+    const double xs = ldexp(m, r + 1);                   // x' = x 2^(-10k) in [1, 2^10)
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float sf = __builtin_amdgcn_exp2f(-0.1f * __builtin_amdgcn_logf((float)xs));
+#else
+    const float sf = exp2f(-0.1f * log2f((float)xs));
+#endif
+    double y = (double)sf;
+    #pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double y2 = y * y, y4 = y2 * y2, y8 = y4 * y4;
+        const double t = xs * (y8 * y2);                 // x' y^10 ~ 1
+        y = y + y * ((1.0 - t) * 0.1);                   // y (1 + (1 - t)/10)
+    }
+    return ldexp(y, -k);
+}
+
+// sqrt(x) for finite x > 0, ~1 ulp: reciprocal square root estimate + Newton (no division).
+CTR_HD double sqrt_rsq(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rsq(x);
+#else
+    double r = 1.0 / sqrt(x);
+#endif
+    r = r * fma(-0.5 * x, r * r, 1.5);
+    double s = x * r;
+    return fma(0.5 * r, fma(-s, s, x), s);
+}
+
 // x^y for x > 0 through exp2/log2 (step-size factors only; a few ulp).
 CTR_HD double powpos(double x, double y)
 {
