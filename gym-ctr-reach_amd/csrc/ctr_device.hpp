@@ -120,6 +120,24 @@ __device__ __forceinline__ double sel9(const double a[9], int k)
     return r;
 }
 
+// A tube system as staged in LDS: the table plus the per-segment divisions precomputed once per
+// workgroup (kz_j = EI_j / GJ_j, model.py:97; inv[m] = 1 / sum of the EI present in mask m,
+// model.py:83), so segment starts never divide.
+struct SysK : ctr_system_t {
+    double kz[3];
+    double inv[8];
+};
+
+__device__ __forceinline__ void sysk_derive(SysK &s, int j)
+{
+    if (j < 3) s.kz[j] = s.EI[j] / s.GJ[j];
+    else if (j < 11) {
+        const int m = j - 3;
+        const double e0 = (m & 1) ? s.EI[0] : 0.0, e1 = (m & 2) ? s.EI[1] : 0.0, e2 = (m & 4) ? s.EI[2] : 0.0;
+        s.inv[m] = 1.0 / ((e0 + e1) + e2);
+    }
+}
+
 // Per-segment RHS constants.  w* = EI_j * U*_j exactly as the reference's left-to-right
 // product ei[j] * ux_0[j] (model.py:85-90); kz = EI/GJ (model.py:97).
 struct SegPar {
@@ -127,25 +145,21 @@ struct SegPar {
     uint32_t present;  // bit j: tube j present (EI_j != 0)
 };
 
-__device__ __forceinline__ SegPar seg_par(const ctr_system_t &sy, uint32_t bits6)
+__device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6)
 {
     SegPar p;
-    double esum = 0.0;
-    double ei[3];
     #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        bool pres = (bits6 >> j) & 1u;
-        bool curv = (bits6 >> (3 + j)) & 1u;
-        ei[j] = pres ? sy.EI[j] : 0.0;
-        double gj = pres ? sy.GJ[j] : 1.0;
+        const bool pres = (bits6 >> j) & 1u;
+        const bool curv = (bits6 >> (3 + j)) & 1u;
+        const double ei = pres ? sy.EI[j] : 0.0;
         p.ux0[j] = curv ? sy.Ux[j] : 0.0;
         p.uy0[j] = curv ? sy.Uy[j] : 0.0;
-        p.wx[j] = ei[j] * p.ux0[j];
-        p.wy[j] = ei[j] * p.uy0[j];
-        p.kz[j] = pres ? ei[j] / gj : 0.0;
+        p.wx[j] = ei * p.ux0[j];
+        p.wy[j] = ei * p.uy0[j];
+        p.kz[j] = pres ? sy.kz[j] : 0.0;
     }
-    esum = (ei[0] + ei[1]) + ei[2];
-    p.inv = 1.0 / esum;
+    p.inv = sy.inv[bits6 & 7u];
     p.present = (uint32_t)(bits6 & 7u);
     return p;
 }
@@ -278,7 +292,7 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
 
 // Forward kinematics of one lane: joints (f32, promoted to f64 as model.py:51) -> tip (f64).
 template <bool HAS_UY>
-__device__ void fk_lane(const ctr_system_t &sy, const float q[6], double tip[3], FkStats &st)
+__device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats &st)
 {
     using namespace rk;
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};

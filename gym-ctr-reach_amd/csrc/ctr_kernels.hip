@@ -54,19 +54,22 @@ struct KCfg {
     int32_t has_uy;
 };
 
-__device__ __forceinline__ void stage_systems(const KCfg &kc, ctr_system_t *lds)
+__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds)
 {
+    constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
     const double *src = reinterpret_cast<const double *>(kc.c.systems);
-    double *dst = reinterpret_cast<double *>(lds);
-    const int nd = kc.c.n_systems * (int)(sizeof(ctr_system_t) / sizeof(double));
-    for (int i = threadIdx.x; i < nd; i += blockDim.x) dst[i] = src[i];
+    const int nd = kc.c.n_systems * ND;
+    for (int i = threadIdx.x; i < nd; i += blockDim.x)
+        reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND]))[i % ND] = src[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < kc.c.n_systems * 11; i += blockDim.x) sysk_derive(lds[i / 11], i % 11);
     __syncthreads();
 }
 
 __device__ __forceinline__ int clamp_sys(int s, int n) { return (s < 0 || s >= n) ? 0 : s; }
 
 template <bool HAS_UY>
-__device__ __forceinline__ void fk_dispatch(const ctr_system_t &sy, const float q[6], double tip[3], FkStats &st)
+__device__ __forceinline__ void fk_dispatch(const SysK &sy, const float q[6], double tip[3], FkStats &st)
 {
     fk_lane<HAS_UY>(sy, q, tip, st);
 }
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
                                                  double *__restrict__ tip, uint32_t *__restrict__ stats,
                                                  uint32_t *__restrict__ status)
 {
-    __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     stage_systems(kc, s_sys);
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (e >= n) return;
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict
                                                          const int32_t *__restrict__ sys_idx,
                                                          const float *__restrict__ actions, int64_t n)
 {
-    __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     stage_systems(kc, s_sys);
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (e >= n) return;
@@ -152,7 +155,7 @@ template <bool HAS_UY>
 __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
                                                    ctr_step_out_t o, int32_t autoreset)
 {
-    __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     stage_systems(kc, s_sys);
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool live = e < b.n;
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
     uint32_t pooled_r = 0;
     if (live) {
         const int s = clamp_sys(b.system[e], kc.c.n_systems);
-        const ctr_system_t &sy = s_sys[s];
+        const SysK &sy = s_sys[s];
         float q[6], a[6];
         #pragma unroll
         for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
@@ -261,14 +264,14 @@ struct ResetOut {
 };
 
 template <bool HAS_UY>
-__device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const ctr_system_t *s_sys, bool active, bool odd,
+__device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys, bool active, bool odd,
                                                uint64_t genv, uint32_t r, const float *q_cur, const double *goal,
                                                int sys_fixed)
 {
     const uint64_t seed = kc.c.seed;
     const int ns = kc.c.n_systems;
     const int s = !active ? 0 : (sys_fixed >= 0 ? sys_fixed : sample_system(seed, r, genv, ns));
-    const ctr_system_t &sy = s_sys[s];
+    const SysK &sy = s_sys[s];
     uint32_t stat = 0;
     float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     double tip[3] = {0.0, 0.0, 0.0};
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
                                                     const int32_t *__restrict__ sys_in, float *__restrict__ obs,
                                                     uint32_t *__restrict__ status)
 {
-    __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ int s_count;
     if (threadIdx.x == 0) {
         s_count = (mode == 0) ? min(*miss_counter(b), (int32_t)b.n) : 0;
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
 template <bool HAS_UY>
 __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
-    __shared__ ctr_system_t s_sys[CTR_MAX_SYSTEMS];
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ int64_t s_count;
     if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
     stage_systems(kc, s_sys);
