@@ -133,6 +133,7 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
     if (status) status[e] = st.status;
 }
 
+
 __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict__ joints,
                                                          const int32_t *__restrict__ sys_idx,
                                                          const float *__restrict__ actions, int64_t n)
