@@ -28,6 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
 FLOP_RHS = 102          # 3 angle differences, ux/uy (10 FMA per tube), u_z' (4/tube), R [u]x (27)
 FLOP_ATTEMPT = 1050     # stage combinations 15x18 FMA, y_new 5x18, error 6x18, scale + norm
 FLOP_SEGMENT = 150      # select_initial_step arithmetic
+FLOP_RK4_STEP = 252     # RK4: 3 stage inputs 3x18 FMA + y_new 18 x 5 (+ stage sums), per step
 FLOP_STEP_EXTRA = 220   # 10 x set_action (160) + reward/obs (60)
 SINCOS_RHS = 3
 PEAK_FP64_VALU = 78.6   # TFLOP/s, MI355X FP64 vector (spec)
@@ -40,7 +41,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=65536, help="environments per GPU")
+    ap.add_argument("--config", type=int, default=3, choices=(2, 3, 5),
+                    help="BASELINE.json config (1-based): 3 = headline (65 536 envs, compliant, scipy RK45); "
+                         "2 = 4 096 envs, rigid model, fixed-step RK4 (h = 10 mm); "
+                         "5 = 65 536 envs, compliant, fixed-step RK4 at h = 2.5 mm (4x finer)")
+    ap.add_argument("--envs", type=int, default=None, help="environments per GPU (default: the config's)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -70,18 +75,33 @@ def make_actions(env, k, seed):
             for _ in range(k)]
 
 
+CONFIGS = {
+    2: dict(envs=4096, integrator="rk4", rk4_steps_per_m=100, model="rigid",
+            text="configs[1]: %d envs/GPU, 3-tube torsionally-rigid CTR, fixed-step RK4 (h = 10 mm) fp64"),
+    3: dict(envs=65536, integrator="rk45_scipy", rk4_steps_per_m=100, model="compliant",
+            text="configs[2]: %d envs/GPU, 3-tube torsionally-compliant CTR, scipy-RK45 (rtol 1e-3, atol 1e-6) fp64"),
+    5: dict(envs=65536, integrator="rk4", rk4_steps_per_m=400, model="compliant",
+            text="configs[4]: %d envs/GPU, 3-tube torsionally-compliant CTR, fixed-step RK4 (h = 2.5 mm, 4x finer) "
+                 "fp64"),
+}
+
+
 def fk_work(env, joints):
     """Algorithmic FP64 flops + sincos of one FK per env at the given joints (device counters)."""
     _, st = env.forward_kinematics(joints, env.system, return_stats=True)
     nfev = st["nfev"].double()
     att = (st["nstep"] + st["nrej"]).double()
     seg = st["nseg"].double()
-    flops = (nfev * FLOP_RHS + att * FLOP_ATTEMPT + seg * FLOP_SEGMENT).sum().item() + FLOP_STEP_EXTRA * joints.shape[0]
+    if env.integrator == "rk4":
+        per = nfev * FLOP_RHS + att * FLOP_RK4_STEP
+    else:
+        per = nfev * FLOP_RHS + att * FLOP_ATTEMPT + seg * FLOP_SEGMENT
+    flops = per.sum().item() + FLOP_STEP_EXTRA * joints.shape[0]
     sincos = (nfev * SINCOS_RHS).sum().item()
     return flops, sincos, nfev.mean().item()
 
 
-def cpu_baseline(args, env_kwargs):
+def cpu_baseline(args, cfgd):
     """Oracle (C port, OpenMP) on this host: env-steps/s on a bounded sample of the workload."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -90,7 +110,8 @@ def cpu_baseline(args, env_kwargs):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     n = 4096
     q, _ = oracle.sample_joints(n, seed=args.seed, stream=1)
-    dg = oracle.fk(oracle.sample_joints(n, seed=args.seed, stream=0)[0])["tip"]
+    dg = oracle.fk(oracle.sample_joints(n, seed=args.seed, stream=0)[0], integrator=cfgd["integrator"],
+                   steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"])["tip"]
     rng = np.random.default_rng(args.seed + 1)
     hi = np.array([1e-3] * 3 + [np.deg2rad(5)] * 3, np.float32)
     t = np.zeros(n, np.int32)
@@ -98,7 +119,8 @@ def cpu_baseline(args, env_kwargs):
     t0 = time.perf_counter()
     while True:
         a = ((rng.random((n, 6)) * 2 - 1) * hi).astype(np.float32)
-        r = oracle.step(q, a, dg, t, 0.020)
+        r = oracle.step(q, a, dg, t, 0.020, integrator=cfgd["integrator"], steps_per_m=cfgd["rk4_steps_per_m"],
+                        model=cfgd["model"])
         q, t = r["joints"], r["t"]
         t[t >= 150] = 0
         steps += 1
@@ -106,8 +128,8 @@ def cpu_baseline(args, env_kwargs):
         if el >= args.cpu_seconds:
             break
     return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "%d envs x %d steps of oracle/ctr_oracle.c (scipy-faithful RK45, fp64), OpenMP %d threads, "
-                      "%.1f s" % (n, steps, threads, el)}
+            "sample": "%d envs x %d steps of oracle/ctr_oracle.c (%s, %s model, fp64), OpenMP %d threads, "
+                      "%.1f s" % (n, steps, cfgd["integrator"], cfgd["model"], threads, el)}
 
 
 def main():
@@ -118,8 +140,10 @@ def main():
     from ctr_reach_amd import distributed as D
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    n = args.envs
-    env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False)
+    cfgd = CONFIGS[args.config]
+    n = args.envs or cfgd["envs"]
+    env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
+                         integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"])
     env.reset()
     acts = make_actions(env, 8, args.seed + rank)
     stream = torch.cuda.current_stream()
@@ -180,9 +204,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: Philox-sampled joints/goals (sample_goal region), uniform actions in the action box",
-        "config": {"workload": "configs[2]: %d envs/GPU, 3-tube torsionally-compliant CTR, scipy-RK45 (rtol 1e-3, "
-                               "atol 1e-6) fp64, system 0, n_substeps 10, tol 0.020, max 150 steps, auto-reset"
-                               % n,
+        "config": {"workload": (cfgd["text"] % n) + ", system 0, n_substeps 10, tol 0.020, max 150 steps, "
+                                                     "auto-reset",
+                   "integrator": cfgd["integrator"], "model": cfgd["model"],
+                   "rk4_steps_per_m": cfgd["rk4_steps_per_m"] if cfgd["integrator"] == "rk4" else None,
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws},
         "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": PEAK_FP64_VALU, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_VALU, "traffic": None,
@@ -196,10 +221,10 @@ def main():
     if os.path.exists(tr):
         with open(tr) as fh:
             t = json.load(fh)
-        if t.get("envs") == n:
+        if t.get("envs") == n and t.get("config", 3) == args.config:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
     if not args.no_cpu_baseline and ws == 1:
-        out["cpu_baseline"] = cpu_baseline(args, {})
+        out["cpu_baseline"] = cpu_baseline(args, cfgd)
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -145,7 +145,7 @@ struct SegPar {
     uint32_t present;  // bit j: tube j present (EI_j != 0)
 };
 
-__device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6)
+__device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool rigid = false)
 {
     SegPar p;
     #pragma unroll
@@ -157,7 +157,7 @@ __device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6)
         p.uy0[j] = curv ? sy.Uy[j] : 0.0;
         p.wx[j] = ei * p.ux0[j];
         p.wy[j] = ei * p.uy0[j];
-        p.kz[j] = pres ? sy.kz[j] : 0.0;
+        p.kz[j] = (pres && !rigid) ? sy.kz[j] : 0.0;   // torsionally rigid: GJ -> infinity
     }
     p.inv = sy.inv[bits6 & 7u];
     p.present = (uint32_t)(bits6 & 7u);
@@ -290,9 +290,11 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
     rcol[0] = R[2]; rcol[1] = R[5]; rcol[2] = R[8];
 }
 
-// Forward kinematics of one lane: joints (f32, promoted to f64 as model.py:51) -> tip (f64).
-template <bool HAS_UY>
-__device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats &st)
+// Forward kinematics of one lane, scipy-RK45 integrator: joints (f64; the env's float32 joints
+// promoted exactly as model.py:51 does) -> tip (f64).  RIGID: torsionally rigid variant (GJ -> inf:
+// u_z stays 0, the tube angles stay at their joint values, so the trig is computed once).
+template <bool HAS_UY, bool RIGID>
+__device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st)
 {
     using namespace rk;
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};
@@ -335,7 +337,7 @@ __device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
-            p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u));
+            p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), RIGID);
             const double endk = end_lds[k * CTR_BLOCK];
             const double a = prev_end, b = endk - 1e-6;          // model.py:141 linspace endpoints
             const double t0 = fmin(a, b);
@@ -386,7 +388,7 @@ __device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats
             Stage f1;
             double f1r[3];
             {
-                const Trig t1 = trig_of(a1);
+                const Trig t1 = RIGID ? ty : trig_of(a1);
                 rhs_core<HAS_UY>(p, t1, u1, R1, f1.uz, f1.R);
                 stage_at(p, t1, u1, R1, f1, f1r);
             }
@@ -453,7 +455,7 @@ __device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats
                 ai[i] = EXPR_A;                                                                \
             }                                                                                  \
             _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = EXPR_R;                      \
-            const Trig tt = trig_of(ai);                                                       \
+            const Trig tt = RIGID ? ty : trig_of(ai);                                          \
             rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
             stage_at(p, tt, ui, Ri, KOUT, rc);                                                 \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
@@ -497,7 +499,7 @@ __device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats
         }
         Stage K6;
         double k6r[3];
-        const Trig tn = trig_of(na);
+        const Trig tn = RIGID ? ty : trig_of(na);
         rhs_core<HAS_UY>(p, tn, nu, nR, K6.uz, K6.R);
         stage_at(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
@@ -554,6 +556,91 @@ __device__ void fk_lane(const SysK &sy, const float q[6], double tip[3], FkStats
     st.nrej = (uint32_t)c_tail;
     st.nseg = (uint32_t)(t_end - t_begin);
 #endif
+    tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
+    if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fixed-step classical RK4 of the same ODE (throughput / convergence mode, BASELINE configs 2
+// and 5).  Each kept segment span [t0, tb] (the same spans as the RK45 path) is split into
+// n = max(1, ceil((tb - t0) * steps_per_m)) equal steps.  Lanes stay in lock-step: one loop
+// iteration = one RK4 step of whichever segment the lane is in.
+// ------------------------------------------------------------------------------------------
+template <bool HAS_UY, bool RIGID>
+__device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], FkStats &st, double steps_per_m)
+{
+    const double beta[3] = {q[0], q[1], q[2]};
+    __shared__ double s_end4[9][CTR_BLOCK];
+    double *end_lds = &s_end4[0][threadIdx.x];
+    const Seg sg = seg_build(sy, beta, end_lds);
+    double yu[3] = {0.0, 0.0, 0.0};
+    double ya[3] = {q[3], q[4], q[5]};
+    double yr[3] = {0.0, 0.0, 0.0};
+    double yR[9];
+    {
+        double s0, c0;
+        ctr_math::sincos_cw(ya[0], &s0, &c0);
+        yR[0] = c0; yR[1] = -s0; yR[2] = 0.0;
+        yR[3] = s0; yR[4] = c0;  yR[5] = 0.0;
+        yR[6] = 0.0; yR[7] = 0.0; yR[8] = 1.0;
+    }
+    const Trig tconst = trig_of(ya);     // RIGID: the tube angles never change
+    SegPar p;
+    double h = 0.0, prev_end = 0.0;
+    int left = 0;                        // RK4 steps left in the current segment
+    uint32_t remaining = sg.kept;
+    for (;;) {
+        if (left == 0) {
+            if (remaining == 0) break;
+            const int k = __builtin_ctz(remaining);
+            remaining &= remaining - 1u;
+            p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), RIGID);
+            const double endk = end_lds[k * CTR_BLOCK];
+            const double a = prev_end, b = endk - 1e-6;
+            const double len = fmax(a, b) - fmin(a, b);
+            prev_end = endk;
+            st.nseg++;
+            left = (len > 0.0) ? max(1, (int)ceil(len * steps_per_m)) : 0;
+            h = (left > 0) ? len / left : 0.0;
+            continue;
+        }
+        Stage k1, k2, k3, k4;
+        double r1[3], r2[3], r3[3], r4[3];
+        double ui[3], ai[3], Ri[9];
+        {
+            const Trig tt = RIGID ? tconst : trig_of(ya);
+            rhs_core<HAS_UY>(p, tt, yu, yR, k1.uz, k1.R);
+            stage_at(p, tt, yu, yR, k1, r1);
+        }
+        const double h2 = 0.5 * h;
+#define CTR_RK4_STAGE(KIN, KOUT, ROUT, C)                                                      \
+        {                                                                                      \
+            _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
+                ui[i] = fma(KIN.uz[i], C, yu[i]);                                              \
+                ai[i] = fma(KIN.al[i], C, ya[i]);                                              \
+            }                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = fma(KIN.R[i], C, yR[i]);     \
+            const Trig tt = RIGID ? tconst : trig_of(ai);                                      \
+            rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
+            stage_at(p, tt, ui, Ri, KOUT, ROUT);                                               \
+        }
+        CTR_RK4_STAGE(k1, k2, r2, h2)
+        CTR_RK4_STAGE(k2, k3, r3, h2)
+        CTR_RK4_STAGE(k3, k4, r4, h)
+#undef CTR_RK4_STAGE
+        const double h6 = h * (1.0 / 6.0);
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            yu[i] = fma(h6, k1.uz[i] + 2.0 * (k2.uz[i] + k3.uz[i]) + k4.uz[i], yu[i]);
+            ya[i] = fma(h6, k1.al[i] + 2.0 * (k2.al[i] + k3.al[i]) + k4.al[i], ya[i]);
+            yr[i] = fma(h6, r1[i] + 2.0 * (r2[i] + r3[i]) + r4[i], yr[i]);
+        }
+        #pragma unroll
+        for (int i = 0; i < 9; ++i) yR[i] = fma(h6, k1.R[i] + 2.0 * (k2.R[i] + k3.R[i]) + k4.R[i], yR[i]);
+        st.nfev += 4;
+        st.nstep++;
+        --left;
+    }
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 }

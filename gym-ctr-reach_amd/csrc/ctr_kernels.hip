@@ -51,7 +51,7 @@ int hip_check(const char *what)
 // Kernel-argument copy of the config (by value, <= 1.2 KB of kernarg).
 struct KCfg {
     ctr_env_config_t c;
-    int32_t has_uy;
+    int32_t mode;       // fk_dispatch MODE bits
 };
 
 __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds)
@@ -68,10 +68,15 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds)
 
 __device__ __forceinline__ int clamp_sys(int s, int n) { return (s < 0 || s >= n) ? 0 : s; }
 
-template <bool HAS_UY>
-__device__ __forceinline__ void fk_dispatch(const SysK &sy, const float q[6], double tip[3], FkStats &st)
+// MODE bits: 1 = some tube has y pre-curvature, 2 = fixed-step RK4 (else scipy RK45),
+// 4 = torsionally rigid model.
+template <int MODE>
+__device__ __forceinline__ void fk_dispatch(const KCfg &kc, const SysK &sy, const float q[6], double tip[3],
+                                            FkStats &st)
 {
-    fk_lane<HAS_UY>(sy, q, tip, st);
+    const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
+    if (MODE & 2) fk_lane_rk4<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st, (double)kc.c.rk4_steps_per_m);
+    else fk_lane<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st);
 }
 
 // Wave-aggregated append of `n_items` int32 per active lane to a list (one atomic per wave).
@@ -105,7 +110,7 @@ __device__ __forceinline__ void write_obs(float *dst, const float ob[14], bool m
 }
 
 // ------------------------------------------------------------------------------------------
-template <bool HAS_UY>
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__ joints,
                                                  const int32_t *__restrict__ sys_idx, int64_t n,
                                                  double *__restrict__ tip, uint32_t *__restrict__ stats,
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
     const int s = sys_idx ? clamp_sys(sys_idx[e], kc.c.n_systems) : 0;
     FkStats st = {0, 0, 0, 0, 0};
     double out[3];
-    fk_dispatch<HAS_UY>(s_sys[s], q, out, st);
+    fk_dispatch<MODE>(kc, s_sys[s], q, out, st);
     #pragma unroll
     for (int i = 0; i < 3; ++i) tip[3 * e + i] = out[i];
     if (stats) {
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict
 }
 
 // ------------------------------------------------------------------------------------------
-template <bool HAS_UY>
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
                                                    ctr_step_out_t o, int32_t autoreset)
 {
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
 #ifdef CTR_EXP_NOFK
         ag[0] = q[0]; ag[1] = q[1]; ag[2] = q[2];      // experiment: step overhead without the FK
 #else
-        fk_dispatch<HAS_UY>(sy, q, ag, st);
+        fk_dispatch<MODE>(kc, sy, q, ag, st);
 #endif
         const int32_t t = b.t[e] + 1;
         double dg[3];
@@ -264,7 +269,7 @@ struct ResetOut {
     uint32_t stat;
 };
 
-template <bool HAS_UY>
+template <int MODE>
 __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys, bool active, bool odd,
                                                uint64_t genv, uint32_t r, const float *q_cur, const double *goal,
                                                int sys_fixed)
@@ -289,7 +294,7 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
             for (int k = 0; k < 3; ++k) tip[k] = goal[k];
         } else {
             FkStats st = {0, 0, 0, 0, 0};
-            fk_dispatch<HAS_UY>(sy, qv, tip, st);
+            fk_dispatch<MODE>(kc, sy, qv, tip, st);
             stat |= st.status;
         }
     }
@@ -314,7 +319,7 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
 // Synchronous reset.  mode 0: envs queued in b.work by k_step (pool misses / no pool), swept
 // grid-stride by a small grid; it also zeroes the miss counter of the next step.
 // mode 1: all envs (or mask).  The pair's odd lane writes the env.
-template <bool HAS_UY>
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mode, const uint8_t *__restrict__ mask,
                                                     const double *__restrict__ goal,
                                                     const int32_t *__restrict__ sys_in, float *__restrict__ obs,
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
     #pragma unroll
     for (int k = 0; k < 6; ++k) qc[k] = active ? b.joints[6 * ee + k] : 0.f;
     const int sf = (active && sys_in) ? clamp_sys(sys_in[ee], kc.c.n_systems) : -1;
-    const ResetOut ro = reset_pair<HAS_UY>(kc, s_sys, active, odd, (uint64_t)(b.env_base + ee), r, qc,
+    const ResetOut ro = reset_pair<MODE>(kc, s_sys, active, odd, (uint64_t)(b.env_base + ee), r, qc,
                                            goal ? goal + 3 * ee : nullptr, sf);
     bool queue = false;
     if (active && odd) {
@@ -391,7 +396,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
 }
 
 // Pool refill: entries (env, reset number) from b.refill, two lanes per entry.
-template <bool HAS_UY>
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         const uint32_t r = active ? (uint32_t)b.refill[2 + 2 * i] : 0;
         const int64_t ps = active ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
         const bool fresh = active && b.pool_r[ps] != r;
-        const ResetOut ro = reset_pair<HAS_UY>(kc, s_sys, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
+        const ResetOut ro = reset_pair<MODE>(kc, s_sys, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
                                                nullptr, -1);
         if (fresh && odd) {
             #pragma unroll
@@ -440,7 +445,11 @@ int check_cfg(const ctr_env_config_t *cfg)
     if (!cfg) return fail(CTR_EINVAL, "cfg is NULL");
     if (cfg->n_systems < 1 || cfg->n_systems > CTR_MAX_SYSTEMS) return fail(CTR_EINVAL, "n_systems out of range");
     if (cfg->n_substeps < 0) return fail(CTR_EINVAL, "n_substeps < 0");
-    if (cfg->integrator != CTR_INTEGRATOR_RK45_SCIPY) return fail(CTR_EINVAL, "integrator not supported yet");
+    if (cfg->integrator != CTR_INTEGRATOR_RK45_SCIPY && cfg->integrator != CTR_INTEGRATOR_RK4)
+        return fail(CTR_EINVAL, "unknown integrator");
+    if (cfg->integrator == CTR_INTEGRATOR_RK4 && cfg->rk4_steps_per_m <= 0)
+        return fail(CTR_EINVAL, "RK4 needs rk4_steps_per_m > 0");
+    if (cfg->model != CTR_MODEL_COMPLIANT && cfg->model != CTR_MODEL_RIGID) return fail(CTR_EINVAL, "unknown model");
     return 0;
 }
 
@@ -461,21 +470,30 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 {
     KCfg kc;
     memcpy(&kc.c, cfg, sizeof *cfg);
-    kc.has_uy = 0;
+    int has_uy = 0;
     for (int s = 0; s < cfg->n_systems; ++s)
         for (int i = 0; i < 3; ++i)
-            if (cfg->systems[s].Uy[i] != 0.0) kc.has_uy = 1;
+            if (cfg->systems[s].Uy[i] != 0.0) has_uy = 1;
+    kc.mode = has_uy | (cfg->integrator == CTR_INTEGRATOR_RK4 ? 2 : 0) | (cfg->model == CTR_MODEL_RIGID ? 4 : 0);
     return kc;
 }
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
-template <typename KT, typename... Args>
-void launch2(bool has_uy, KT kf, KT kt, dim3 g, hipStream_t s, Args... args)
-{
-    if (has_uy) hipLaunchKernelGGL(kt, g, dim3(BLOCK), 0, s, args...);
-    else hipLaunchKernelGGL(kf, g, dim3(BLOCK), 0, s, args...);
-}
+// Launch kernel template K<MODE> for the runtime mode (8 instantiations).
+#define CTR_LAUNCH(K, MODE, GRID, STREAM, ...)                                                     \
+    do {                                                                                           \
+        switch (MODE) {                                                                            \
+        case 0: hipLaunchKernelGGL(K<0>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        case 1: hipLaunchKernelGGL(K<1>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        case 2: hipLaunchKernelGGL(K<2>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        case 3: hipLaunchKernelGGL(K<3>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        case 4: hipLaunchKernelGGL(K<4>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        case 5: hipLaunchKernelGGL(K<5>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        case 6: hipLaunchKernelGGL(K<6>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
+        default: hipLaunchKernelGGL(K<7>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;       \
+        }                                                                                          \
+    } while (0)
 
 }  // namespace
 
@@ -492,8 +510,7 @@ int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env
     if (n < 0 || (n > 0 && (!joints || !tip))) return fail(CTR_EINVAL, "ctr_fk: bad buffers");
     if (n == 0) return 0;
     KCfg kc = make_kcfg(cfg);
-    launch2(kc.has_uy != 0, k_fk<false>, k_fk<true>, dim3(grid_for(n)), (hipStream_t)stream, kc, joints, sys_idx, n,
-            tip, stats, status);
+    CTR_LAUNCH(k_fk, kc.mode, dim3(grid_for(n)), (hipStream_t)stream, kc, joints, sys_idx, n, tip, stats, status);
     return hip_check("ctr_fk launch");
 }
 
@@ -523,13 +540,13 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    launch2(kc.has_uy != 0, k_step<false>, k_step<true>, dim3(grid_for(b.n)), s, kc, b, actions, o, autoreset);
+    CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(b.n)), s, kc, b, actions, o, autoreset);
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset) {
         // misses are rare with a pool: a small grid sweeps the list grid-stride
         const unsigned g = b.pool_depth > 0 ? std::min(grid_for(2 * b.n), 64u) : grid_for(2 * b.n);
-        launch2(kc.has_uy != 0, k_reset<false>, k_reset<true>, dim3(g), s, kc, b, 0,
-                (const uint8_t *)nullptr, (const double *)nullptr, (const int32_t *)nullptr, o.obs, o.status);
+        CTR_LAUNCH(k_reset, kc.mode, dim3(g), s, kc, b, 0, (const uint8_t *)nullptr, (const double *)nullptr,
+                   (const int32_t *)nullptr, o.obs, o.status);
         return hip_check("ctr_step reset launch");
     }
     return 0;
@@ -545,8 +562,8 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
     if (b.n == 0) return 0;
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
-    launch2(kc.has_uy != 0, k_reset<false>, k_reset<true>, dim3(grid_for(2 * b.n)), (hipStream_t)stream, kc, b, 1,
-            mask, goal, system, obs, status);
+    CTR_LAUNCH(k_reset, kc.mode, dim3(grid_for(2 * b.n)), (hipStream_t)stream, kc, b, 1, mask, goal, system, obs,
+               status);
     return hip_check("ctr_reset launch");
 }
 
@@ -561,7 +578,7 @@ int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void 
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
     // grid covers one entry per env (2 lanes each); larger queues are swept grid-stride
-    launch2(kc.has_uy != 0, k_refill<false>, k_refill<true>, dim3(grid_for(2 * b.n)), s, kc, b);
+    CTR_LAUNCH(k_refill, kc.mode, dim3(grid_for(2 * b.n)), s, kc, b);
     if (int r = hip_check("ctr_pool_refill launch")) return r;
     hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.refill);
     return hip_check("ctr_pool_refill clear");

@@ -10,10 +10,12 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 3
+CTR_ABI_VERSION = 4
 CTR_MAX_SYSTEMS = 8
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1
+CTR_MODEL_COMPLIANT = 0
+CTR_MODEL_RIGID = 1
 CTR_STATUS_STEP_UNDERFLOW = 1
 CTR_STATUS_SAMPLER_STUCK = 2
 CTR_STATUS_NAN = 4
@@ -36,6 +38,8 @@ class CtrEnvConfig(ctypes.Structure):
         ("resample_joints", ctypes.c_int32),
         ("integrator", ctypes.c_int32),
         ("rk4_steps_per_m", ctypes.c_int32),
+        ("model", ctypes.c_int32),
+        ("model_pad", ctypes.c_int32),
         ("tol", ctypes.c_double),
         ("seed", ctypes.c_uint64),
         ("systems", CtrSystem * CTR_MAX_SYSTEMS),

@@ -33,7 +33,8 @@ class CtrReachEnv(GoalEnvBase):
     def __init__(self, ctr_systems_parameters, goal_tolerance_parameters, noise_parameters, joint_representation,
                  initial_joints, constrain_alpha, extension_action_limit, rotation_action_limit,
                  max_steps_per_episode, n_substeps, evaluation, select_systems, resample_joints=True,
-                 length_based_sample=False, domain_rand=0.0, device="cuda", seed=0):
+                 length_based_sample=False, domain_rand=0.0, device="cuda", seed=0, integrator="rk45_scipy",
+                 rk4_steps_per_m=100, model="compliant"):
         kw = dict(ctr_systems_parameters=ctr_systems_parameters, goal_tolerance_parameters=goal_tolerance_parameters,
                   noise_parameters=noise_parameters, joint_representation=joint_representation,
                   initial_joints=initial_joints, constrain_alpha=constrain_alpha,
@@ -41,7 +42,8 @@ class CtrReachEnv(GoalEnvBase):
                   max_steps_per_episode=max_steps_per_episode, n_substeps=n_substeps, evaluation=evaluation,
                   select_systems=select_systems, resample_joints=resample_joints,
                   length_based_sample=length_based_sample, domain_rand=domain_rand)
-        self.vec = CtrReachVecEnv(1, device=device, seed=seed, autoreset=False, **kw)
+        self.vec = CtrReachVecEnv(1, device=device, seed=seed, autoreset=False, integrator=integrator,
+                                  rk4_steps_per_m=rk4_steps_per_m, model=model, **kw)
         v = self.vec
         self.select_systems = v.select_systems
         self.ctr_system_parameters = v.ctr_system_parameters

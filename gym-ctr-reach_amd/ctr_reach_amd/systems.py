@@ -102,7 +102,7 @@ def to_ctr_system(tubes):
 
 def make_config(systems, n_substeps=10, max_steps=150, constrain_alpha=False, egocentric=True,
                 resample_joints=True, tol=0.020, seed=0, integrator=_abi.CTR_INTEGRATOR_RK45_SCIPY,
-                rk4_steps_per_m=0):
+                rk4_steps_per_m=0, model=_abi.CTR_MODEL_COMPLIANT):
     """Build the ctr_env_config_t for a list of [Tube x3] systems (already filtered)."""
     if not 1 <= len(systems) <= _abi.CTR_MAX_SYSTEMS:
         raise ValueError("between 1 and %d systems are supported" % _abi.CTR_MAX_SYSTEMS)
@@ -115,6 +115,7 @@ def make_config(systems, n_substeps=10, max_steps=150, constrain_alpha=False, eg
     cfg.resample_joints = int(bool(resample_joints))
     cfg.integrator = int(integrator)
     cfg.rk4_steps_per_m = int(rk4_steps_per_m)
+    cfg.model = int(model)
     cfg.tol = float(tol)
     cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     for k, tubes in enumerate(systems):
@@ -124,3 +125,20 @@ def make_config(systems, n_substeps=10, max_steps=150, constrain_alpha=False, eg
 
 def copy_config(cfg):
     return copy.copy(cfg)
+
+
+INTEGRATORS = {"rk45_scipy": _abi.CTR_INTEGRATOR_RK45_SCIPY, "rk4": _abi.CTR_INTEGRATOR_RK4}
+MODELS = {"compliant": _abi.CTR_MODEL_COMPLIANT, "rigid": _abi.CTR_MODEL_RIGID}
+
+
+def solver_codes(integrator, rk4_steps_per_m, model):
+    """Validate the build's solver kwargs (integrator / h / model as explicit
+    extra kwargs) and return their ABI codes."""
+    if integrator not in INTEGRATORS:
+        raise ValueError("integrator must be one of %s" % sorted(INTEGRATORS))
+    if model not in MODELS:
+        raise ValueError("model must be one of %s" % sorted(MODELS))
+    spm = int(rk4_steps_per_m)
+    if integrator == "rk4" and spm <= 0:
+        raise ValueError("rk4_steps_per_m must be > 0")
+    return INTEGRATORS[integrator], spm, MODELS[model]

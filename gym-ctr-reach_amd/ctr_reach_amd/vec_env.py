@@ -21,7 +21,7 @@ import numpy as np
 from . import _abi
 from .goal_tolerance import GoalTolerance
 from .spaces import Box, Dict
-from .systems import default_kwargs, make_config, tubes_from_params
+from .systems import default_kwargs, make_config, solver_codes, tubes_from_params
 
 NUM_TUBES = 3
 EXT_TOL = 1e-3    # obs.py:14
@@ -76,10 +76,16 @@ def action_space(extension_action_limit, rotation_action_limit):
 class CtrReachVecEnv(object):
     """Batched CTR-Reach on one GPU.  Constructor kwargs = the reference's (ctr_reach_env.py:14-17)
     plus ``num_envs``, ``device``, ``seed``, ``env_base`` (global id of env 0 for sharding),
-    ``autoreset``.  Missing reference kwargs take the CTR-Reach-v0 registration defaults."""
+    ``autoreset``.  Missing reference kwargs take the CTR-Reach-v0 registration defaults.
+
+    Solver kwargs (build-specific): ``integrator`` "rk45_scipy" (default; the
+    reference's solve_ivp RK45, bit-for-bit in its step sequence) or "rk4" (fixed step,
+    ``rk4_steps_per_m`` equal steps per metre of each segment); ``model`` "compliant" (the
+    reference's torsionally-compliant ODE, model.py:72-117) or "rigid" (GJ -> infinity)."""
 
     def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
-                 pool_depth=None, refill_interval=32, **kwargs):
+                 pool_depth=None, refill_interval=32, integrator="rk45_scipy", rk4_steps_per_m=100,
+                 model="compliant", **kwargs):
         torch = _torch()
         kw = default_kwargs()
         kw.update(kwargs)
@@ -90,6 +96,8 @@ class CtrReachVecEnv(object):
             raise NotImplementedError("per-env domain randomisation is a later round (SURVEY 8f #4)")
         assert kw["joint_representation"] in ("egocentric", "proprioceptive")
         self.kwargs = kw
+        self.integrator, self.rk4_steps_per_m, self.model = integrator, int(rk4_steps_per_m), model
+        solver = solver_codes(integrator, rk4_steps_per_m, model)
         self.lib = _abi.load()
         self.num_envs = int(num_envs)
         self.device = torch.device(device)
@@ -116,7 +124,8 @@ class CtrReachVecEnv(object):
                                max_steps=self.max_steps_per_episode, constrain_alpha=self.constrain_alpha,
                                egocentric=self.joint_representation == "egocentric",
                                resample_joints=self.resample_joints, tol=self.goal_tolerance.get_tol(),
-                               seed=self.seed_value)
+                               seed=self.seed_value, integrator=solver[0], rk4_steps_per_m=solver[1],
+                               model=solver[2])
         n, dev = self.num_envs, self.device
         f32, f64, i32 = torch.float32, torch.float64, torch.int32
         init = np.asarray(kw["initial_joints"], dtype=np.float64)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 3
+#define CTR_ABI_VERSION 4
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -60,6 +60,10 @@ typedef struct ctr_system_t {
 #define CTR_INTEGRATOR_RK45_SCIPY 0    /* scipy solve_ivp RK45 emulation, rtol 1e-3 atol 1e-6 (parity) */
 #define CTR_INTEGRATOR_RK4        1    /* fixed-step classical RK4 of the same ODE (throughput)       */
 
+/* Mechanics model */
+#define CTR_MODEL_COMPLIANT 0          /* torsionally compliant (the reference, model.py:72-117)        */
+#define CTR_MODEL_RIGID     1          /* torsionally rigid: GJ -> infinity, tube angles constant       */
+
 /* Environment configuration (registration kwargs, ctr_reach_envs/__init__.py:6-94). */
 typedef struct ctr_env_config_t {
     int32_t n_systems;          /* len(select_systems), 1..CTR_MAX_SYSTEMS              */
@@ -69,7 +73,9 @@ typedef struct ctr_env_config_t {
     int32_t egocentric;         /* joint_representation == 'egocentric'                  */
     int32_t resample_joints;    /* resample_joints                                       */
     int32_t integrator;         /* CTR_INTEGRATOR_*                                      */
-    int32_t rk4_steps_per_m;    /* RK4 only: steps per metre of arclength                */
+    int32_t rk4_steps_per_m;    /* RK4 only: steps per metre of arclength (> 0)          */
+    int32_t model;              /* CTR_MODEL_*                                           */
+    int32_t model_pad;
     double  tol;                /* goal_tolerance.get_tol()                              */
     uint64_t seed;              /* Philox key for resets                                 */
     ctr_system_t systems[CTR_MAX_SYSTEMS];

@@ -15,6 +15,15 @@ typedef struct {
 
 void oracle_fk(const float *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
                double *tip, int32_t *nfev, int32_t *nstep, int32_t *nseg, int32_t *status);
+void oracle_fk_ex(const float *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
+                  int integrator, int steps_per_m, int rigid,
+                  double *tip, int32_t *nfev, int32_t *nstep, int32_t *nseg, int32_t *status);
+void oracle_step_ex(int64_t n, const oracle_system_t *systems, const int32_t *sys_idx,
+                    float *joints, const float *actions, const double *desired, int32_t *t,
+                    const double *tol, int n_substeps, int max_steps, int constrain_alpha,
+                    int multi, int egocentric, int integrator, int steps_per_m, int rigid,
+                    double *achieved, double *obs, double *reward,
+                    uint8_t *done, uint8_t *success, double *error, int32_t *nfev);
 void oracle_step(int64_t n, const oracle_system_t *systems, const int32_t *sys_idx,
                  float *joints, const float *actions, const double *desired, int32_t *t,
                  const double *tol, int n_substeps, int max_steps, int constrain_alpha,

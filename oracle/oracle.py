@@ -38,9 +38,10 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         i64, i32, u64, u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32
-        L.oracle_fk.argtypes = [P, P, i64, P, P, P, P, P, P]
-        L.oracle_step.argtypes = [i64, P, P, P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P]
+        ci = ctypes.c_int
+        L.oracle_fk_ex.argtypes = [P, P, i64, P, ci, ci, ci, P, P, P, P, P]
+        L.oracle_step_ex.argtypes = [i64, P, P, P, P, P, P, P, ci, ci, ci, ci, ci, ci, ci, ci,
+                                     P, P, P, P, P, P, P]
         L.oracle_set_action.argtypes = [i64, P, P, P, P, ctypes.c_int, ctypes.c_int]
         L.oracle_sample_joints.argtypes = [i64, P, P, u64, P, u32, i64, P, P]
         L.oracle_philox.argtypes = [P, u64]
@@ -81,8 +82,22 @@ def make_systems(params=None, select=None):
     return arr
 
 
-def fk(joints, system=None, systems=None):
-    """Batched Model.forward_kinematics (model.py:30).  Returns dict of tip/nfev/nstep/nseg/status."""
+INTEGRATORS = {"rk45_scipy": 0, "rk4": 1}
+MODELS = {"compliant": 0, "rigid": 1}
+
+
+def _fkopts(integrator, steps_per_m, model):
+    it = INTEGRATORS[integrator] if isinstance(integrator, str) else int(integrator)
+    rg = MODELS[model] if isinstance(model, str) else int(model)
+    if it == 1 and int(steps_per_m) <= 0:
+        raise ValueError("rk4 needs steps_per_m > 0")
+    return it, int(steps_per_m), rg
+
+
+def fk(joints, system=None, systems=None, integrator="rk45_scipy", steps_per_m=0, model="compliant"):
+    """Batched Model.forward_kinematics (model.py:30).  Returns dict of tip/nfev/nstep/nseg/status.
+    integrator="rk4" / model="rigid" select the build's fixed-step / torsionally-rigid modes."""
+    it, spm, rg = _fkopts(integrator, steps_per_m, model)
     q = np.ascontiguousarray(joints, dtype=np.float32).reshape(-1, 6)
     n = q.shape[0]
     s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
@@ -90,14 +105,16 @@ def fk(joints, system=None, systems=None):
     tip = np.zeros((n, 3))
     nfev = np.zeros(n, np.int32); nstep = np.zeros(n, np.int32)
     nseg = np.zeros(n, np.int32); status = np.zeros(n, np.int32)
-    lib().oracle_fk(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), _p(tip), _p(nfev), _p(nstep),
-                    _p(nseg), _p(status))
+    lib().oracle_fk_ex(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), it, spm, rg, _p(tip), _p(nfev),
+                       _p(nstep), _p(nseg), _p(status))
     return dict(tip=tip, nfev=nfev, nstep=nstep, nseg=nseg, status=status)
 
 
 def step(joints, actions, desired, t, tol, system=None, systems=None, n_substeps=10, max_steps=150,
-         constrain_alpha=False, multi=False, egocentric=True):
+         constrain_alpha=False, multi=False, egocentric=True, integrator="rk45_scipy", steps_per_m=0,
+         model="compliant"):
     """Batched CtrReachEnv.step (ctr_reach_env.py:124-158); returns new state + outputs."""
+    it, spm, rg = _fkopts(integrator, steps_per_m, model)
     q = np.array(joints, dtype=np.float32).reshape(-1, 6)
     n = q.shape[0]
     a = np.ascontiguousarray(np.broadcast_to(actions, (n, 6)), dtype=np.float32)
@@ -110,9 +127,9 @@ def step(joints, actions, desired, t, tol, system=None, systems=None, n_substeps
     ag = np.zeros((n, 3)); obs = np.zeros((n, olen)); rew = np.zeros(n)
     done = np.zeros(n, np.uint8); succ = np.zeros(n, np.uint8); err = np.zeros(n)
     nfev = np.zeros(n, np.int32)
-    lib().oracle_step(n, ctypes.cast(systems, ctypes.c_void_p), _p(s), _p(q), _p(a), _p(dg), _p(tt), _p(tl),
-                      n_substeps, max_steps, int(constrain_alpha), int(multi), int(egocentric),
-                      _p(ag), _p(obs), _p(rew), _p(done), _p(succ), _p(err), _p(nfev))
+    lib().oracle_step_ex(n, ctypes.cast(systems, ctypes.c_void_p), _p(s), _p(q), _p(a), _p(dg), _p(tt), _p(tl),
+                         n_substeps, max_steps, int(constrain_alpha), int(multi), int(egocentric), it, spm, rg,
+                         _p(ag), _p(obs), _p(rew), _p(done), _p(succ), _p(err), _p(nfev))
     return dict(joints=q, t=tt, achieved_goal=ag, observation=obs, reward=rew, done=done.astype(bool),
                 is_success=succ.astype(bool), error=err, nfev=nfev)
 

@@ -1,6 +1,16 @@
+# GPU round: parity tests, smoke, bench (headline + configs 2 and 5).  Stops at the first
+# step that ends abnormally (fault / abort / time limit); test failures (rc 1) continue.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" 
-tail -30 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -3 gpurun_out/smoke.log
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 --cpu-seconds 5 > gpurun_out/bench.log 2>&1; echo "bench rc=$?"; tail -3 gpurun_out/bench.log
+run() {   # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"; tail -${TAILN:-4} "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "abnormal exit, stopping"; exit $rc; fi
+}
+TAILN=30 run pytest_gpu 600 python -m pytest tests -m gpu -q
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+run bench 400 python bench.py --steps 20 --warmup 5 --cpu-seconds 5
+run bench_c2 300 python bench.py --config 2 --steps 20 --warmup 5 --cpu-seconds 5
+run bench_c5 300 python bench.py --config 5 --steps 20 --warmup 5 --cpu-seconds 5

@@ -1,0 +1,59 @@
+"""Oracle checks for the build's extra solver modes (BASELINE.json configs 2 and 5).
+
+Fixed-step RK4 and the torsionally-rigid model have no reference counterpart.  What is pinned:
+- RK4 (compliant model) against the reference's RK45 fixtures.  The gap is the reference's own
+  rtol-1e-3 integration error (SURVEY.md section 8 note (a)).  It stays under the north_star
+  bar of 1e-4 m except on about 0.03 % of system-2 cases.
+- RK4 converges: halving h changes the tip by O(h^4).
+- rigid RK4 and rigid RK45 agree to the RK45 tolerance.
+- rigid == compliant when every tube's torsional stiffness is scaled to infinity.
+"""
+import os
+
+import numpy as np
+import pytest
+
+
+def _d(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+@pytest.mark.parametrize("name", ["fk_random.npz", "fk_edge.npz", "csv_known.npz"])
+def test_rk4_vs_reference_rk45(golden_dir, oracle_mod, name):
+    d = _d(golden_dir, name)
+    ref = d["tip"] if "tip" in d.files else d["tip_reference"]
+    got = oracle_mod.fk(d["joints"], d["system"], integrator="rk4", steps_per_m=100)
+    err = np.linalg.norm(got["tip"] - ref, axis=1)
+    assert err.max() < 1.5e-4, err.max()
+    assert (err <= 1e-4).mean() >= 0.999
+    # RK4 makes ceil(len * 100) steps of 4 RHS per segment
+    assert (got["nfev"] % 4 == 0).all() and (got["status"] == 0).all()
+
+
+def test_rk4_converges(golden_dir, oracle_mod):
+    d = _d(golden_dir, "fk_random.npz")
+    q, s = d["joints"][:200], d["system"][:200]
+    t1 = oracle_mod.fk(q, s, integrator="rk4", steps_per_m=50)["tip"]
+    t2 = oracle_mod.fk(q, s, integrator="rk4", steps_per_m=100)["tip"]
+    t4 = oracle_mod.fk(q, s, integrator="rk4", steps_per_m=200)["tip"]
+    e12 = np.abs(t1 - t2).max()
+    e24 = np.abs(t2 - t4).max()
+    assert e24 < e12 / 8, (e12, e24)          # fourth order: ratio about 16
+
+
+def test_rigid_rk4_vs_rigid_rk45(oracle_mod):
+    q, _ = oracle_mod.sample_joints(500, seed=11, stream=1)
+    a = oracle_mod.fk(q, integrator="rk4", steps_per_m=400, model="rigid")["tip"]
+    b = oracle_mod.fk(q, integrator="rk45_scipy", model="rigid")["tip"]
+    assert np.abs(a - b).max() < 1e-4
+
+
+def test_rigid_is_infinite_torsional_stiffness_limit(oracle_mod):
+    q, _ = oracle_mod.sample_joints(300, seed=12, stream=1)
+    rigid = oracle_mod.fk(q, integrator="rk4", steps_per_m=200, model="rigid")["tip"]
+    stiff = oracle_mod.make_systems()
+    for k in range(len(stiff)):
+        for i in range(3):
+            stiff[k].G[i] *= 1e12
+    comp = oracle_mod.fk(q, systems=stiff, integrator="rk4", steps_per_m=200)["tip"]
+    assert np.abs(rigid - comp).max() < 1e-9
