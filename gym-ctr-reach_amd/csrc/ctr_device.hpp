@@ -766,4 +766,51 @@ __device__ __forceinline__ int sample_system(uint64_t seed, uint32_t epoch, uint
     return s < n_systems ? s : n_systems - 1;
 }
 
+// Domain randomisation: the tube table of reset `epoch` of env `env` (Model.randomize_parameters,
+// model.py:20-28; sample_parameters / randomize_value, model_utils.py:5-35; Tube.__init__,
+// Tube.py:7-19).  Per tube j, five uniforms u[5j .. 5j+4] from Philox stream 3 re-sample
+// (d_in, d_out, E, G, U_x) as numpy's uniform(low, high) = low + (high - low) * u with
+// low = v - v*rand, high = v + v*rand; L, L_c and U_y keep their values (randomisation 0).
+// d^4 is (d*d)*(d*d) (the reference uses math.pow; <= 1 ulp apart), I = pi d4 / 64,
+// J = pi d4 / 32, EI = E*I, GJ = G*J.
+__device__ __forceinline__ void domain_system(const ctr_system_t &base, const ctr_tube_raw_t &raw, double rnd,
+                                              uint64_t seed, uint32_t epoch, uint64_t env, ctr_system_t &out,
+                                              ctr_tube_raw_t *raw_out)
+{
+#pragma clang fp contract(off)
+    double u[16];
+    #pragma unroll
+    for (int blk = 0; blk < 8; ++blk) {
+        uint32_t c[4] = {(uint32_t)blk, epoch, (uint32_t)env, (uint32_t)(env >> 32) ^ (3u << 24)};
+        philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        u[2 * blk] = u53(c[0], c[1]);
+        u[2 * blk + 1] = u53(c[2], c[3]);
+    }
+    #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double v[5] = {raw.Din[j], raw.Dout[j], raw.E[j], raw.G[j], base.Ux[j]};
+        #pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const double lo = v[k] - v[k] * rnd, hi = v[k] + v[k] * rnd;
+            v[k] = lo + (hi - lo) * u[5 * j + k];
+        }
+        const double di2 = v[0] * v[0], do2 = v[1] * v[1];
+        const double d4 = do2 * do2 - di2 * di2;
+        const double J = (3.141592653589793 * d4) / 32.0;
+        const double I = (3.141592653589793 * d4) / 64.0;
+        out.L[j] = base.L[j];
+        out.Lc[j] = base.Lc[j];
+        out.EI[j] = v[2] * I;
+        out.GJ[j] = v[3] * J;
+        out.Ux[j] = v[4];
+        out.Uy[j] = base.Uy[j];
+        if (raw_out) {
+            raw_out->Din[j] = v[0];
+            raw_out->Dout[j] = v[1];
+            raw_out->E[j] = v[2];
+            raw_out->G[j] = v[3];
+        }
+    }
+}
+
 }  // namespace ctr

@@ -10,6 +10,7 @@
 //                 for the queued / masked envs                        (envs/ctr_reach_env.py:70-114)
 //   k_refill      precomputes queued resets into the pool, two lanes per reset
 //   k_reward      compute_reward over a batch                          (envs/ctr_reach_env.py:160-170)
+//   k_domain_params  each env's current (domain-randomised) tube table  (envs/model.py:20-28)
 //
 // Work lists (auto-reset misses, pool refills) are appended with one wave-aggregated atomic per
 // wave.  The tube tables (<= 8 systems x 18 doubles) travel as a kernel argument and are staged
@@ -54,19 +55,48 @@ struct KCfg {
     int32_t mode;       // fk_dispatch MODE bits
 };
 
-__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds)
+__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr)
 {
     constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
     const double *src = reinterpret_cast<const double *>(kc.c.systems);
     const int nd = kc.c.n_systems * ND;
     for (int i = threadIdx.x; i < nd; i += blockDim.x)
         reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND]))[i % ND] = src[i];
+    if (raw_lds) {
+        constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
+        const double *rs = reinterpret_cast<const double *>(kc.c.raw);
+        for (int i = threadIdx.x; i < kc.c.n_systems * NR; i += blockDim.x)
+            reinterpret_cast<double *>(raw_lds)[i] = rs[i];
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < kc.c.n_systems * 11; i += blockDim.x) sysk_derive(lds[i / 11], i % 11);
     __syncthreads();
 }
 
 __device__ __forceinline__ int clamp_sys(int s, int n) { return (s < 0 || s >= n) ? 0 : s; }
+
+// Per-lane tube tables for domain randomisation: dynamic LDS, BLOCK entries (launched with
+// lane_lds_bytes(kc), 0 when randomisation is off).
+extern __shared__ SysK s_lane_dyn[];
+
+__host__ __device__ inline size_t lane_lds_bytes(const KCfg &kc)
+{
+    return kc.c.domain_rand != 0.0 ? (size_t)BLOCK * sizeof(SysK) : 0;
+}
+
+// The tube table episode `epoch` of env `genv` integrates with: the system row, or with domain
+// randomisation the lane's re-sampled table (epoch 0 = before the first reset: the nominal
+// table, as the reference constructor's FK, ctr_reach_env.py:65).
+__device__ __forceinline__ const SysK &episode_sys(const KCfg &kc, const SysK *s_sys, const ctr_tube_raw_t *s_raw,
+                                                   int s, uint32_t epoch, uint64_t genv)
+{
+    if (kc.c.domain_rand == 0.0 || epoch == 0) return s_sys[s];
+    SysK &me = s_lane_dyn[threadIdx.x];
+    domain_system(s_sys[s], s_raw[s], kc.c.domain_rand, kc.c.seed, epoch, genv, me, nullptr);
+    #pragma unroll
+    for (int j = 0; j < 11; ++j) sysk_derive(me, j);
+    return me;
+}
 
 // MODE bits: 1 = some tube has y pre-curvature, 2 = fixed-step RK4 (else scipy RK45),
 // 4 = torsionally rigid model.
@@ -110,9 +140,11 @@ __device__ __forceinline__ void write_obs(float *dst, const float ob[14], bool m
 }
 
 // ------------------------------------------------------------------------------------------
+// tables != NULL: row e integrates with its own tube table tables[e] (staged per lane in LDS).
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__ joints,
-                                                 const int32_t *__restrict__ sys_idx, int64_t n,
+                                                 const int32_t *__restrict__ sys_idx,
+                                                 const ctr_system_t *__restrict__ tables, int64_t n,
                                                  double *__restrict__ tip, uint32_t *__restrict__ stats,
                                                  uint32_t *__restrict__ status)
 {
@@ -124,9 +156,17 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
     #pragma unroll
     for (int i = 0; i < 6; ++i) q[i] = joints[6 * e + i];
     const int s = sys_idx ? clamp_sys(sys_idx[e], kc.c.n_systems) : 0;
+    const SysK *sy = &s_sys[s];
+    if (tables) {
+        SysK &me = s_lane_dyn[threadIdx.x];
+        static_cast<ctr_system_t &>(me) = tables[e];
+        #pragma unroll
+        for (int j = 0; j < 11; ++j) sysk_derive(me, j);
+        sy = &me;
+    }
     FkStats st = {0, 0, 0, 0, 0};
     double out[3];
-    fk_dispatch<MODE>(kc, s_sys[s], q, out, st);
+    fk_dispatch<MODE>(kc, *sy, q, out, st);
     #pragma unroll
     for (int i = 0; i < 3; ++i) tip[3 * e + i] = out[i];
     if (stats) {
@@ -162,7 +202,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
                                                    ctr_step_out_t o, int32_t autoreset)
 {
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
-    stage_systems(kc, s_sys);
+    __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
+    stage_systems(kc, s_sys, s_raw);
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool live = e < b.n;
     bool miss = false;       // done, but no pooled reset available -> k_reset
@@ -180,7 +221,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
 #ifdef CTR_EXP_NOFK
         ag[0] = q[0]; ag[1] = q[1]; ag[2] = q[2];      // experiment: step overhead without the FK
 #else
-        fk_dispatch<MODE>(kc, sy, q, ag, st);
+        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);
 #endif
         const int32_t t = b.t[e] + 1;
         double dg[3];
@@ -270,7 +311,8 @@ struct ResetOut {
 };
 
 template <int MODE>
-__device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys, bool active, bool odd,
+__device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys, const ctr_tube_raw_t *s_raw,
+                                               bool active, bool odd,
                                                uint64_t genv, uint32_t r, const float *q_cur, const double *goal,
                                                int sys_fixed)
 {
@@ -294,7 +336,7 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
             for (int k = 0; k < 3; ++k) tip[k] = goal[k];
         } else {
             FkStats st = {0, 0, 0, 0, 0};
-            fk_dispatch<MODE>(kc, sy, qv, tip, st);
+            fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, r, genv), qv, tip, st);
             stat |= st.status;
         }
     }
@@ -326,12 +368,13 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
                                                     uint32_t *__restrict__ status)
 {
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
+    __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int s_count;
     if (threadIdx.x == 0) {
         s_count = (mode == 0) ? min(*miss_counter(b), (int32_t)b.n) : 0;
         if (mode == 0 && blockIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;   // next step's counter
     }
-    stage_systems(kc, s_sys);
+    stage_systems(kc, s_sys, s_raw);
     const int64_t stride = (mode == 0) ? (int64_t)gridDim.x * (BLOCK / 2) : (int64_t)1 << 62;
     for (int64_t base = (int64_t)blockIdx.x * (BLOCK / 2); mode != 0 || base < s_count; base += stride) {
     const int64_t slot = base + (threadIdx.x >> 1);
@@ -349,7 +392,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
     #pragma unroll
     for (int k = 0; k < 6; ++k) qc[k] = active ? b.joints[6 * ee + k] : 0.f;
     const int sf = (active && sys_in) ? clamp_sys(sys_in[ee], kc.c.n_systems) : -1;
-    const ResetOut ro = reset_pair<MODE>(kc, s_sys, active, odd, (uint64_t)(b.env_base + ee), r, qc,
+    const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, active, odd, (uint64_t)(b.env_base + ee), r, qc,
                                            goal ? goal + 3 * ee : nullptr, sf);
     bool queue = false;
     if (active && odd) {
@@ -400,9 +443,10 @@ template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
+    __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int64_t s_count;
     if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
-    stage_systems(kc, s_sys);
+    stage_systems(kc, s_sys, s_raw);
     const int64_t per_grid = (int64_t)gridDim.x * (BLOCK / 2);
     for (int64_t base = (int64_t)blockIdx.x * (BLOCK / 2); base < s_count; base += per_grid) {
         const int64_t i = base + (threadIdx.x >> 1);
@@ -412,7 +456,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         const uint32_t r = active ? (uint32_t)b.refill[2 + 2 * i] : 0;
         const int64_t ps = active ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
         const bool fresh = active && b.pool_r[ps] != r;
-        const ResetOut ro = reset_pair<MODE>(kc, s_sys, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
+        const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
                                                nullptr, -1);
         if (fresh && odd) {
             #pragma unroll
@@ -424,6 +468,28 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             b.pool_r[ps] = r;
         }
     }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_domain_params(KCfg kc, ctr_batch_t b, ctr_system_t *__restrict__ sys_out,
+                                                            ctr_tube_raw_t *__restrict__ raw_out)
+{
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
+    __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
+    stage_systems(kc, s_sys, s_raw);
+    const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= b.n) return;
+    const int s = clamp_sys(b.system[e], kc.c.n_systems);
+    const uint32_t ep = b.epoch[e];
+    ctr_system_t sy;
+    ctr_tube_raw_t raw;
+    if (kc.c.domain_rand != 0.0 && ep != 0) {
+        domain_system(s_sys[s], s_raw[s], kc.c.domain_rand, kc.c.seed, ep, (uint64_t)(b.env_base + e), sy, &raw);
+    } else {
+        sy = s_sys[s];
+        raw = s_raw[s];
+    }
+    if (sys_out) sys_out[e] = sy;
+    if (raw_out) raw_out[e] = raw;
 }
 
 __global__ __launch_bounds__(64) void k_clear_counter(int32_t *counter)
@@ -450,6 +516,7 @@ int check_cfg(const ctr_env_config_t *cfg)
     if (cfg->integrator == CTR_INTEGRATOR_RK4 && cfg->rk4_steps_per_m <= 0)
         return fail(CTR_EINVAL, "RK4 needs rk4_steps_per_m > 0");
     if (cfg->model != CTR_MODEL_COMPLIANT && cfg->model != CTR_MODEL_RIGID) return fail(CTR_EINVAL, "unknown model");
+    if (!isfinite(cfg->domain_rand)) return fail(CTR_EINVAL, "domain_rand must be finite");
     return 0;
 }
 
@@ -481,17 +548,17 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
 // Launch kernel template K<MODE> for the runtime mode (8 instantiations).
-#define CTR_LAUNCH(K, MODE, GRID, STREAM, ...)                                                     \
+#define CTR_LAUNCH(K, MODE, GRID, SHM, STREAM, ...)                                                     \
     do {                                                                                           \
         switch (MODE) {                                                                            \
-        case 0: hipLaunchKernelGGL(K<0>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        case 1: hipLaunchKernelGGL(K<1>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        case 2: hipLaunchKernelGGL(K<2>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        case 3: hipLaunchKernelGGL(K<3>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        case 4: hipLaunchKernelGGL(K<4>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        case 5: hipLaunchKernelGGL(K<5>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        case 6: hipLaunchKernelGGL(K<6>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;        \
-        default: hipLaunchKernelGGL(K<7>, GRID, dim3(BLOCK), 0, STREAM, __VA_ARGS__); break;       \
+        case 0: hipLaunchKernelGGL(K<0>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        case 1: hipLaunchKernelGGL(K<1>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        case 2: hipLaunchKernelGGL(K<2>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        case 3: hipLaunchKernelGGL(K<3>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        case 4: hipLaunchKernelGGL(K<4>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        case 5: hipLaunchKernelGGL(K<5>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        case 6: hipLaunchKernelGGL(K<6>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;        \
+        default: hipLaunchKernelGGL(K<7>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;       \
         }                                                                                          \
     } while (0)
 
@@ -503,15 +570,30 @@ int ctr_abi_version(void) { return CTR_ABI_VERSION; }
 
 const char *ctr_last_error(void) { return g_err; }
 
-int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg, double *tip,
-           uint32_t *stats, uint32_t *status, void *stream)
+static int fk_impl(const float *joints, const int32_t *sys_idx, const ctr_system_t *tables, int64_t n,
+                   const ctr_env_config_t *cfg, double *tip, uint32_t *stats, uint32_t *status, void *stream)
 {
     if (int r = check_cfg(cfg)) return r;
     if (n < 0 || (n > 0 && (!joints || !tip))) return fail(CTR_EINVAL, "ctr_fk: bad buffers");
     if (n == 0) return 0;
     KCfg kc = make_kcfg(cfg);
-    CTR_LAUNCH(k_fk, kc.mode, dim3(grid_for(n)), (hipStream_t)stream, kc, joints, sys_idx, n, tip, stats, status);
+    if (tables) kc.mode |= 1;     // per-row tables may carry y pre-curvature
+    CTR_LAUNCH(k_fk, kc.mode, dim3(grid_for(n)), tables ? (size_t)BLOCK * sizeof(SysK) : 0, (hipStream_t)stream, kc,
+               joints, sys_idx, tables, n, tip, stats, status);
     return hip_check("ctr_fk launch");
+}
+
+int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg, double *tip,
+           uint32_t *stats, uint32_t *status, void *stream)
+{
+    return fk_impl(joints, sys_idx, nullptr, n, cfg, tip, stats, status, stream);
+}
+
+int ctr_fk_tables(const float *joints, const ctr_system_t *tables, int64_t n, const ctr_env_config_t *cfg,
+                  double *tip, uint32_t *stats, uint32_t *status, void *stream)
+{
+    if (n > 0 && !tables) return fail(CTR_EINVAL, "ctr_fk_tables: tables is NULL");
+    return fk_impl(joints, nullptr, tables, n, cfg, tip, stats, status, stream);
 }
 
 int ctr_set_action(const ctr_env_config_t *cfg, float *joints, const int32_t *sys_idx, const float *actions,
@@ -540,12 +622,12 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(b.n)), s, kc, b, actions, o, autoreset);
+    CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(b.n)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset) {
         // misses are rare with a pool: a small grid sweeps the list grid-stride
         const unsigned g = b.pool_depth > 0 ? std::min(grid_for(2 * b.n), 64u) : grid_for(2 * b.n);
-        CTR_LAUNCH(k_reset, kc.mode, dim3(g), s, kc, b, 0, (const uint8_t *)nullptr, (const double *)nullptr,
+        CTR_LAUNCH(k_reset, kc.mode, dim3(g), lane_lds_bytes(kc), s, kc, b, 0, (const uint8_t *)nullptr, (const double *)nullptr,
                    (const int32_t *)nullptr, o.obs, o.status);
         return hip_check("ctr_step reset launch");
     }
@@ -562,7 +644,7 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
     if (b.n == 0) return 0;
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
-    CTR_LAUNCH(k_reset, kc.mode, dim3(grid_for(2 * b.n)), (hipStream_t)stream, kc, b, 1, mask, goal, system, obs,
+    CTR_LAUNCH(k_reset, kc.mode, dim3(grid_for(2 * b.n)), lane_lds_bytes(kc), (hipStream_t)stream, kc, b, 1, mask, goal, system, obs,
                status);
     return hip_check("ctr_reset launch");
 }
@@ -578,10 +660,25 @@ int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void 
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
     // grid covers one entry per env (2 lanes each); larger queues are swept grid-stride
-    CTR_LAUNCH(k_refill, kc.mode, dim3(grid_for(2 * b.n)), s, kc, b);
+    CTR_LAUNCH(k_refill, kc.mode, dim3(grid_for(2 * b.n)), lane_lds_bytes(kc), s, kc, b);
     if (int r = hip_check("ctr_pool_refill launch")) return r;
     hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.refill);
     return hip_check("ctr_pool_refill clear");
+}
+
+int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr_system_t *sys_out,
+                      ctr_tube_raw_t *raw_out, void *stream)
+{
+    if (int rc = check_cfg(cfg)) return rc;
+    if (!batch) return fail(CTR_EINVAL, "batch is NULL");
+    const ctr_batch_t b = *batch;
+    if (b.n < 0 || b.n > 0x7fffffff) return fail(CTR_EINVAL, "batch size out of range");
+    if (b.n == 0 || (!sys_out && !raw_out)) return 0;
+    if (!b.system || !b.epoch) return fail(CTR_EINVAL, "ctr_domain_params: batch needs system and epoch");
+    const KCfg kc = make_kcfg(cfg);
+    hipLaunchKernelGGL(k_domain_params, dim3(grid_for(b.n)), dim3(BLOCK), 0, (hipStream_t)stream, kc, b, sys_out,
+                       raw_out);
+    return hip_check("ctr_domain_params launch");
 }
 
 int ctr_compute_reward(const double *achieved, const double *desired, int64_t n, double tol, float *reward,

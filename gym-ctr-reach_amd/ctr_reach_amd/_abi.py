@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 4
+CTR_ABI_VERSION = 5
 CTR_MAX_SYSTEMS = 8
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1
@@ -28,6 +28,10 @@ class CtrSystem(ctypes.Structure):
     _fields_ = [("L", _d3), ("Lc", _d3), ("EI", _d3), ("GJ", _d3), ("Ux", _d3), ("Uy", _d3)]
 
 
+class CtrTubeRaw(ctypes.Structure):
+    _fields_ = [("Din", _d3), ("Dout", _d3), ("E", _d3), ("G", _d3)]
+
+
 class CtrEnvConfig(ctypes.Structure):
     _fields_ = [
         ("n_systems", ctypes.c_int32),
@@ -43,6 +47,9 @@ class CtrEnvConfig(ctypes.Structure):
         ("tol", ctypes.c_double),
         ("seed", ctypes.c_uint64),
         ("systems", CtrSystem * CTR_MAX_SYSTEMS),
+        ("domain_rand", ctypes.c_double),
+        ("domain_pad", ctypes.c_double),
+        ("raw", CtrTubeRaw * CTR_MAX_SYSTEMS),
     ]
 
 
@@ -91,7 +98,7 @@ class CtrStepOut(ctypes.Structure):
 
 
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
-            "ctr_pool_refill", "ctr_compute_reward")
+            "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables")
 
 _lib = None
 
@@ -119,7 +126,10 @@ def load(path=None):
     L.ctr_reset.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P, _P, _P, _P]
     L.ctr_pool_refill.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P]
     L.ctr_compute_reward.argtypes = [_P, _P, i64, ctypes.c_double, _P, _P]
-    for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward"):
+    L.ctr_domain_params.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P]
+    L.ctr_fk_tables.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), _P, _P, _P, _P]
+    for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward",
+               "ctr_domain_params", "ctr_fk_tables"):
         getattr(L, fn).restype = ctypes.c_int
     if L.ctr_abi_version() != CTR_ABI_VERSION:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))

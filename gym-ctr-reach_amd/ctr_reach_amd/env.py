@@ -22,7 +22,13 @@ class Model(object):
 
     def forward_kinematics(self, joint, system, **kwargs):
         q = np.asarray(joint, dtype=np.float32).reshape(-1, 6)
-        tip = self._env.forward_kinematics(q, np.full(q.shape[0], int(system)))
+        v = self._env
+        if v.kwargs.get("domain_rand", 0.0) != 0.0 and int(system) == int(v.system[0].item()):
+            # the episode's randomised table (Model.current_sys_parameters, model.py:20-28)
+            table = v.domain_parameters()["table"][0:1].expand(q.shape[0], 18)
+            tip = v.forward_kinematics(q, tables=table)
+        else:
+            tip = v.forward_kinematics(q, np.full(q.shape[0], int(system)))
         out = tip.cpu().numpy()
         return out[0] if np.ndim(joint) == 1 else out
 

@@ -100,9 +100,20 @@ def to_ctr_system(tubes):
     return s
 
 
+def to_ctr_tube_raw(tubes):
+    """Tube.__init__ inputs that domain randomisation re-samples (model_utils.py:15-18)."""
+    r = _abi.CtrTubeRaw()
+    for i, t in enumerate(tubes):
+        r.Din[i] = t.diameter_inner
+        r.Dout[i] = t.diameter_outer
+        r.E[i] = t.E
+        r.G[i] = t.G
+    return r
+
+
 def make_config(systems, n_substeps=10, max_steps=150, constrain_alpha=False, egocentric=True,
                 resample_joints=True, tol=0.020, seed=0, integrator=_abi.CTR_INTEGRATOR_RK45_SCIPY,
-                rk4_steps_per_m=0, model=_abi.CTR_MODEL_COMPLIANT):
+                rk4_steps_per_m=0, model=_abi.CTR_MODEL_COMPLIANT, domain_rand=0.0):
     """Build the ctr_env_config_t for a list of [Tube x3] systems (already filtered)."""
     if not 1 <= len(systems) <= _abi.CTR_MAX_SYSTEMS:
         raise ValueError("between 1 and %d systems are supported" % _abi.CTR_MAX_SYSTEMS)
@@ -118,8 +129,10 @@ def make_config(systems, n_substeps=10, max_steps=150, constrain_alpha=False, eg
     cfg.model = int(model)
     cfg.tol = float(tol)
     cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    cfg.domain_rand = float(domain_rand)
     for k, tubes in enumerate(systems):
         cfg.systems[k] = to_ctr_system(tubes)
+        cfg.raw[k] = to_ctr_tube_raw(tubes)
     return cfg
 
 

@@ -92,8 +92,6 @@ class CtrReachVecEnv(object):
         if kw.get("length_based_sample"):
             raise NotImplementedError("length_based_sample: the reference branch is broken "
                                       "(reads the nonexistent self.system_parameters, ctr_reach_env.py:88)")
-        if kw.get("domain_rand", 0.0) != 0.0:
-            raise NotImplementedError("per-env domain randomisation is a later round (SURVEY 8f #4)")
         assert kw["joint_representation"] in ("egocentric", "proprioceptive")
         self.kwargs = kw
         self.integrator, self.rk4_steps_per_m, self.model = integrator, int(rk4_steps_per_m), model
@@ -125,7 +123,7 @@ class CtrReachVecEnv(object):
                                egocentric=self.joint_representation == "egocentric",
                                resample_joints=self.resample_joints, tol=self.goal_tolerance.get_tol(),
                                seed=self.seed_value, integrator=solver[0], rk4_steps_per_m=solver[1],
-                               model=solver[2])
+                               model=solver[2], domain_rand=kw.get("domain_rand", 0.0))
         n, dev = self.num_envs, self.device
         f32, f64, i32 = torch.float32, torch.float64, torch.int32
         init = np.asarray(kw["initial_joints"], dtype=np.float64)
@@ -295,8 +293,10 @@ class CtrReachVecEnv(object):
         d = np.linalg.norm(achieved_goal - desired_goal, axis=-1)
         return -(d > tol).astype(np.float64)
 
-    def forward_kinematics(self, joints, system=None, stream=None, return_stats=False):
-        """Batched Model.forward_kinematics (model.py:30): joints [M,6] -> tip [M,3] f64 (device)."""
+    def forward_kinematics(self, joints, system=None, stream=None, return_stats=False, tables=None):
+        """Batched Model.forward_kinematics (model.py:30): joints [M,6] -> tip [M,3] f64 (device).
+        ``system`` picks rows of the nominal tube tables; ``tables`` (a [M, 18] float64 device tensor
+        in ctr_system_t order, e.g. ``domain_parameters()["table"]``) gives every row its own."""
         torch = _torch()
         q = torch.as_tensor(joints, dtype=torch.float32, device=self.device).reshape(-1, 6).contiguous()
         m = q.shape[0]
@@ -304,12 +304,34 @@ class CtrReachVecEnv(object):
         tip = torch.empty((m, 3), dtype=torch.float64, device=self.device)
         stats = torch.zeros((m, 4), dtype=torch.int32, device=self.device) if return_stats else None
         status = torch.zeros(m, dtype=torch.int32, device=self.device)
-        rc = self.lib.ctr_fk(_abi.ptr(q), _abi.ptr(s), m, self.cfg, _abi.ptr(tip), _abi.ptr(stats), _abi.ptr(status),
-                             _abi.stream_ptr(stream))
-        _abi.check(rc, "ctr_fk")
+        if tables is not None:
+            tb = torch.as_tensor(tables, dtype=torch.float64, device=self.device).reshape(m, 18).contiguous()
+            rc = self.lib.ctr_fk_tables(_abi.ptr(q), _abi.ptr(tb), m, self.cfg, _abi.ptr(tip), _abi.ptr(stats),
+                                        _abi.ptr(status), _abi.stream_ptr(stream))
+            _abi.check(rc, "ctr_fk_tables")
+        else:
+            rc = self.lib.ctr_fk(_abi.ptr(q), _abi.ptr(s), m, self.cfg, _abi.ptr(tip), _abi.ptr(stats),
+                                 _abi.ptr(status), _abi.stream_ptr(stream))
+            _abi.check(rc, "ctr_fk")
         if return_stats:
             return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=stats[:, 2], nseg=stats[:, 3], status=status)
         return tip
+
+    def domain_parameters(self, stream=None):
+        """Each env's current tube table (Model.current_sys_parameters after randomize_parameters,
+        model.py:20-28): dict of [n, 3] float64 device tensors L, L_c, EI, GJ, U_x, U_y,
+        diameter_inner, diameter_outer, E, G, plus "table" ([n, 18], the ctr_system_t rows the FK
+        integrates with).  Without domain randomisation these are the nominal rows."""
+        torch = _torch()
+        n = self.num_envs
+        table = torch.empty((n, 18), dtype=torch.float64, device=self.device)
+        raw = torch.empty((n, 12), dtype=torch.float64, device=self.device)
+        rc = self.lib.ctr_domain_params(self.cfg, self._batch, _abi.ptr(table), _abi.ptr(raw), _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_domain_params")
+        out = {k: table[:, 3 * i:3 * i + 3] for i, k in enumerate(("L", "L_c", "EI", "GJ", "U_x", "U_y"))}
+        out.update({k: raw[:, 3 * i:3 * i + 3] for i, k in enumerate(("diameter_inner", "diameter_outer", "E", "G"))})
+        out["table"] = table
+        return out
 
     def gather_outputs(self, group=None):
         """Optional collective for a single-process trainer: every rank's last-step (tip, reward,

@@ -24,6 +24,9 @@
  *   ctr_reset           CtrReachEnv.reset(goal=None, system=None)         envs/ctr_reach_env.py:70-114
  *                       (+ Obs.sample_goal envs/obs.py:185-207, get_obs obs.py:136-164)
  *   ctr_compute_reward  CtrReachEnv.compute_reward(ag, dg, info)          envs/ctr_reach_env.py:160-170
+ *   ctr_fk_tables       Model.forward_kinematics with per-row tube tables  envs/model.py:30-70
+ *   ctr_domain_params   Model.current_sys_parameters after randomize_parameters
+ *                                                                          envs/model.py:20-28, model_utils.py:5-35
  */
 #ifndef CTR_REACH_AMD_H
 #define CTR_REACH_AMD_H
@@ -34,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 4
+#define CTR_ABI_VERSION 5
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -55,6 +58,15 @@ typedef struct ctr_system_t {
     double Ux[3];      /* pre-curvature x    (Tube.U_x)                  */
     double Uy[3];      /* pre-curvature y    (Tube.U_y)                  */
 } ctr_system_t;
+
+/* Raw tube inputs of Tube.__init__ (envs/CTR_Python/Tube.py:7-19) for one system, needed only
+ * by domain randomisation, which re-samples them every reset (envs/model_utils.py:5-35). */
+typedef struct ctr_tube_raw_t {
+    double Din[3];     /* diameter_inner                                 */
+    double Dout[3];    /* diameter_outer                                 */
+    double E[3];       /* stiffness                                      */
+    double G[3];       /* torsional_stiffness                            */
+} ctr_tube_raw_t;
 
 /* Integrator selection */
 #define CTR_INTEGRATOR_RK45_SCIPY 0    /* scipy solve_ivp RK45 emulation, rtol 1e-3 atol 1e-6 (parity) */
@@ -79,6 +91,14 @@ typedef struct ctr_env_config_t {
     double  tol;                /* goal_tolerance.get_tol()                              */
     uint64_t seed;              /* Philox key for resets                                 */
     ctr_system_t systems[CTR_MAX_SYSTEMS];
+    /* Domain randomisation (domain_rand kwarg; Model.randomize_parameters, model.py:20-28, called
+     * by reset, ctr_reach_env.py:80).  0 = off.  Otherwise every reset draws, per tube, d_in,
+     * d_out, E, G and U_x uniformly in v * [1 - domain_rand, 1 + domain_rand] (L, L_c, U_y are
+     * kept) from Philox stream 3 keyed (seed, global env id, reset number), and the episode's
+     * FKs use the tube table derived from them.  raw[] holds the unrandomised inputs. */
+    double domain_rand;
+    double domain_pad;
+    ctr_tube_raw_t raw[CTR_MAX_SYSTEMS];
 } ctr_env_config_t;
 
 /* Device-resident batch state, row-major per environment ([n][k]). */
@@ -137,6 +157,12 @@ const char *ctr_last_error(void);
 int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg,
            double *tip, uint32_t *stats, uint32_t *status, void *stream);
 
+/* Model.forward_kinematics with one tube table per row: tables [n] (device), e.g. the
+ * domain-randomised tables from ctr_domain_params (the reference integrates with
+ * Model.current_sys_parameters, model.py:13,30).  cfg supplies the integrator and model. */
+int ctr_fk_tables(const float *joints, const ctr_system_t *tables, int64_t n, const ctr_env_config_t *cfg,
+                  double *tip, uint32_t *stats, uint32_t *status, void *stream);
+
 /* n_substeps x Obs.set_action, in place on joints [n][6] (device). */
 int ctr_set_action(const ctr_env_config_t *cfg, float *joints, const int32_t *sys_idx,
                    const float *actions, int64_t n, void *stream);
@@ -157,6 +183,13 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
  * consumed, and by ctr_reset for the P resets after the one it computes), then clear the
  * queue.  Call it every few steps; it is a no-op when the queue is empty. */
 int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
+
+/* The tube table each environment's current episode uses (Model.current_sys_parameters,
+ * model.py:13,20-28): with domain randomisation the episode's re-sampled table, else the
+ * environment's system row.  sys_out [n] (derived, as the FK uses it) and raw_out [n] (the
+ * re-sampled Tube inputs; U_x is in sys_out) may each be NULL.  (device) */
+int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr_system_t *sys_out,
+                      ctr_tube_raw_t *raw_out, void *stream);
 
 /* Batched compute_reward over leading dims: ag, dg [n][3] f64 -> reward [n] f32 in {-1, 0}. */
 int ctr_compute_reward(const double *achieved, const double *desired, int64_t n, double tol,

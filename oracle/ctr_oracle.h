@@ -37,6 +37,9 @@ void oracle_sample_joints(int64_t n, const oracle_system_t *systems, const int32
 void oracle_philox(uint32_t *ctr4, uint64_t seed);
 void oracle_segments(const float *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
                      int32_t *m, double *S);
+void oracle_domain_systems(int64_t n, const oracle_system_t *systems, const double *din, const double *dout,
+                           const int32_t *sys_idx, double rnd, uint64_t seed, const uint32_t *epoch,
+                           int64_t env_base, oracle_system_t *out);
 int oracle_version(void);
 
 #ifdef __cplusplus

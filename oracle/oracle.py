@@ -46,6 +46,7 @@ def lib():
         L.oracle_sample_joints.argtypes = [i64, P, P, u64, P, u32, i64, P, P]
         L.oracle_philox.argtypes = [P, u64]
         L.oracle_segments.argtypes = [P, P, i64, P, P, P]
+        L.oracle_domain_systems.argtypes = [i64, P, P, P, P, ctypes.c_double, u64, P, i64, P]
         _lib = L
     return _lib
 
@@ -92,6 +93,35 @@ def _fkopts(integrator, steps_per_m, model):
     if it == 1 and int(steps_per_m) <= 0:
         raise ValueError("rk4 needs steps_per_m > 0")
     return it, int(steps_per_m), rg
+
+
+def tube_diameters(params=None, select=None):
+    """(d_in, d_out) [n_sys, 3] float64 from a ctr_systems_parameters dict."""
+    params = params or default_system_params()
+    names = list(params.keys())
+    if select is not None:
+        names = [names[i] for i in select]
+    din = np.zeros((len(names), 3)); dout = np.zeros((len(names), 3))
+    for k, name in enumerate(names):
+        for i, tname in enumerate(sorted(params[name].keys())):
+            din[k, i] = params[name][tname]["diameter_inner"]
+            dout[k, i] = params[name][tname]["diameter_outer"]
+    return din, dout
+
+
+def domain_systems(n, rand, seed, epoch, env_base=0, system=None, params=None, select=None):
+    """Per-env OracleSystem array [n]: the tube table of each env's episode `epoch` under domain
+    randomisation (model.py:20-28, model_utils.py:5-35; Philox stream 3).  Use with
+    fk/step(system=np.arange(n), systems=<this>)."""
+    systems = make_systems(params, select)
+    din, dout = tube_diameters(params, select)
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    ep = np.ascontiguousarray(np.broadcast_to(epoch, (n,)), dtype=np.uint32)
+    out = (OracleSystem * n)()
+    lib().oracle_domain_systems(n, ctypes.cast(systems, ctypes.c_void_p), _p(np.ascontiguousarray(din)),
+                                _p(np.ascontiguousarray(dout)), _p(s), float(rand), int(seed) & (2**64 - 1),
+                                _p(ep), int(env_base), ctypes.cast(out, ctypes.c_void_p))
+    return out
 
 
 def fk(joints, system=None, systems=None, integrator="rk45_scipy", steps_per_m=0, model="compliant"):

@@ -243,14 +243,14 @@ def test_facade_gym_surface(cuda):
         env.close()
 
 
-@pytest.mark.parametrize("depth,interval", [(4, 8), (1, 1000), (2, 3)])
-def test_reset_pool_matches_synchronous_resets(cuda, depth, interval):
+@pytest.mark.parametrize("depth,interval,rand", [(4, 8, 0.0), (1, 1000, 0.0), (2, 3, 0.0), (4, 8, 0.05)])
+def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
     """Pooled auto-resets (precomputed ahead of time, consumed by a copy; including pool misses
     that fall back to the synchronous path) give bit-identical trajectories to computing every
     reset at the step that needs it: a reset is a pure function of (seed, env id, reset number)."""
     import torch
     n = 4096
-    kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3])
+    kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3], domain_rand=rand)
     a = _env(cuda, n, pool_depth=0, **kw)
     b = _env(cuda, n, pool_depth=depth, refill_interval=interval, **kw)
     a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03   # plenty of early successes

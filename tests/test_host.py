@@ -48,25 +48,24 @@ def test_abi_rejects_bad_arguments_without_gpu():
 
 
 def test_struct_layout_matches_header(tmp_path):
-    """ctypes mirrors of the ABI structs have the C sizes/offsets (gcc on the header)."""
+    """ctypes mirrors of the ABI structs have the C sizes and every field offset (gcc on the header)."""
     from ctr_reach_amd import _abi
+    structs = [(_abi.CtrSystem, "ctr_system_t"), (_abi.CtrTubeRaw, "ctr_tube_raw_t"),
+               (_abi.CtrEnvConfig, "ctr_env_config_t"), (_abi.CtrBatch, "ctr_batch_t"),
+               (_abi.CtrStepOut, "ctr_step_out_t")]
+    lines, want = [], []
+    for cls, cname in structs:
+        lines.append('  printf("%%zu\\n", sizeof(%s));' % cname)
+        want.append(ctypes.sizeof(cls))
+        for fname, _ in cls._fields_:
+            lines.append('  printf("%%zu\\n", offsetof(%s, %s));' % (cname, fname))
+            want.append(getattr(cls, fname).offset)
     prog = tmp_path / "layout.c"
-    prog.write_text(r'''
-#include <stdio.h>
-#include <stddef.h>
-#include "ctr_reach_amd.h"
-int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(ctr_system_t), sizeof(ctr_env_config_t),
-         offsetof(ctr_env_config_t, tol), offsetof(ctr_env_config_t, systems), sizeof(ctr_batch_t),
-         offsetof(ctr_batch_t, work), sizeof(ctr_step_out_t));
-  return 0; }
-''')
+    prog.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"ctr_reach_amd.h\"\nint main(void) {\n"
+                    + "\n".join(lines) + "\n  return 0; }\n")
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
     got = list(map(int, subprocess.check_output([str(exe)]).split()))
-    want = [ctypes.sizeof(_abi.CtrSystem), ctypes.sizeof(_abi.CtrEnvConfig), _abi.CtrEnvConfig.tol.offset,
-            _abi.CtrEnvConfig.systems.offset, ctypes.sizeof(_abi.CtrBatch), _abi.CtrBatch.work.offset,
-            ctypes.sizeof(_abi.CtrStepOut)]
     assert got == want
 
 

@@ -57,3 +57,19 @@ def test_rigid_is_infinite_torsional_stiffness_limit(oracle_mod):
             stiff[k].G[i] *= 1e12
     comp = oracle_mod.fk(q, systems=stiff, integrator="rk4", steps_per_m=200)["tip"]
     assert np.abs(rigid - comp).max() < 1e-9
+
+
+def test_domain_draws_distribution(oracle_mod):
+    """model_utils.py:27-35: each re-sampled value is uniform on v * [1 - r, 1 + r]; L, L_c, U_y
+    are kept; epoch 0 (before the first reset) is the nominal table."""
+    from scipy import stats
+    n, r = 20000, 0.05
+    ds = oracle_mod.domain_systems(n, r, seed=5, epoch=np.arange(1, n + 1) % 7 + 1)
+    nom = oracle_mod.make_systems()[0]
+    for field in ("E", "G", "Ux"):
+        x = np.array([getattr(ds[i], field)[1] for i in range(n)]) / getattr(nom, field)[1]
+        assert stats.kstest((x - (1 - r)) / (2 * r), "uniform").pvalue > 1e-3, field
+    for field in ("L", "Lc", "Uy"):
+        assert all(getattr(ds[i], field)[2] == getattr(nom, field)[2] for i in range(0, n, 97))
+    d0 = oracle_mod.domain_systems(4, r, seed=5, epoch=0)
+    assert all(d0[i].E[0] == nom.E[0] and d0[i].I[0] == nom.I[0] for i in range(4))
