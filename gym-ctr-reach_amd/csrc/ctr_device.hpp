@@ -353,6 +353,14 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 #endif
             const double interval = tb - t0;
             if (interval == 0.0) continue;                        // OdeSolver.step: t == t_bound
+            if (p.present == 0u) {
+                // a gap with no tube (joints outside the nesting constraints): the reference's
+                // RHS is NaN (1/sum EI = inf, model.py:87-93) and scipy's step loop never ends
+                // on the NaN step size; stop with a NaN tip
+                yr[0] = yr[1] = yr[2] = NAN;
+                st.status |= CTR_STATUS_NAN;
+                break;
+            }
             // select_initial_step (common.py:68-140), order 4, direction +1
             double isc_u[3], isc_a[3], isc_r[3], isc_R[9];
             #pragma unroll

@@ -10,6 +10,7 @@
 //                 for the queued / masked envs                        (envs/ctr_reach_env.py:70-114)
 //   k_refill      precomputes queued resets into the pool, two lanes per reset
 //   k_reward      compute_reward over a batch                          (envs/ctr_reach_env.py:160-170)
+//   k_jacobian    forward-difference tip Jacobian, 7 lanes per env       (CTR_Python/CTR_Model.py:251-262)
 //   k_domain_params  each env's current (domain-randomised) tube table  (envs/model.py:20-28)
 //
 // Work lists (auto-reset misses, pool refills) are appended with one wave-aggregated atomic per
@@ -101,12 +102,20 @@ __device__ __forceinline__ const SysK &episode_sys(const KCfg &kc, const SysK *s
 // MODE bits: 1 = some tube has y pre-curvature, 2 = fixed-step RK4 (else scipy RK45),
 // 4 = torsionally rigid model.
 template <int MODE>
+__device__ __forceinline__ void fk_dispatch_d(const KCfg &kc, const SysK &sy, const double qd[6], double tip[3],
+                                              FkStats &st)
+{
+    if (MODE & 2) fk_lane_rk4<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st, (double)kc.c.rk4_steps_per_m);
+    else fk_lane<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st);
+}
+
+// Model.forward_kinematics widens the float32 joints of Obs to float64 (model.py:48-62).
+template <int MODE>
 __device__ __forceinline__ void fk_dispatch(const KCfg &kc, const SysK &sy, const float q[6], double tip[3],
                                             FkStats &st)
 {
     const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
-    if (MODE & 2) fk_lane_rk4<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st, (double)kc.c.rk4_steps_per_m);
-    else fk_lane<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st);
+    fk_dispatch_d<MODE>(kc, sy, qd, tip, st);
 }
 
 // Wave-aggregated append of `n_items` int32 per active lane to a list (one atomic per wave).
@@ -178,6 +187,50 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
     if (status) status[e] = st.status;
 }
 
+
+// Forward-difference tip Jacobian, SEVEN lanes per environment: lane c < 6 integrates the FK at
+// q + eps e_c, lane 6 at q (CTR_Model.jac, CTR_Python/CTR_Model.py:251-262, applied to this
+// env's FK); the base tip is exchanged through LDS.  36 envs per 256-lane workgroup.
+constexpr int JAC_ENVS = BLOCK / 7;
+
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_jacobian(KCfg kc, const double *__restrict__ joints,
+                                                       const int32_t *__restrict__ sys_idx, int64_t n, double eps,
+                                                       double *__restrict__ tip, double *__restrict__ jac,
+                                                       uint32_t *__restrict__ status)
+{
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
+    __shared__ double s_tip[3][BLOCK];
+    stage_systems(kc, s_sys);
+    const int slot = threadIdx.x / 7, col = threadIdx.x % 7;
+    const int64_t e = (int64_t)blockIdx.x * JAC_ENVS + slot;
+    const bool active = slot < JAC_ENVS && e < n;
+    double r[3] = {0.0, 0.0, 0.0};
+    FkStats st = {0, 0, 0, 0, 0};
+    if (active) {
+        double q[6];
+        #pragma unroll
+        for (int i = 0; i < 6; ++i) q[i] = joints[6 * e + i];
+        #pragma unroll
+        for (int i = 0; i < 6; ++i)
+            if (i == col) q[i] = q[i] + eps;
+        const int s = sys_idx ? clamp_sys(sys_idx[e], kc.c.n_systems) : 0;
+        fk_dispatch_d<MODE>(kc, s_sys[s], q, r, st);
+    }
+    #pragma unroll
+    for (int k = 0; k < 3; ++k) s_tip[k][threadIdx.x] = r[k];
+    __syncthreads();
+    if (!active) return;
+    const int base = slot * 7 + 6;
+    if (col < 6) {
+        #pragma unroll
+        for (int k = 0; k < 3; ++k) jac[18 * e + 6 * k + col] = (r[k] - s_tip[k][base]) / eps;
+    } else if (tip) {
+        #pragma unroll
+        for (int k = 0; k < 3; ++k) tip[3 * e + k] = r[k];
+    }
+    if (status) atomicOr(&status[e], st.status);
+}
 
 __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict__ joints,
                                                          const int32_t *__restrict__ sys_idx,
@@ -594,6 +647,19 @@ int ctr_fk_tables(const float *joints, const ctr_system_t *tables, int64_t n, co
 {
     if (n > 0 && !tables) return fail(CTR_EINVAL, "ctr_fk_tables: tables is NULL");
     return fk_impl(joints, nullptr, tables, n, cfg, tip, stats, status, stream);
+}
+
+int ctr_jacobian(const double *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg, double eps,
+                 double *tip, double *jac, uint32_t *status, void *stream)
+{
+    if (int r = check_cfg(cfg)) return r;
+    if (n < 0 || (n > 0 && (!joints || !jac))) return fail(CTR_EINVAL, "ctr_jacobian: bad buffers");
+    if (!(eps != 0.0) || !isfinite(eps)) return fail(CTR_EINVAL, "ctr_jacobian: eps must be finite and nonzero");
+    if (n == 0) return 0;
+    KCfg kc = make_kcfg(cfg);
+    const unsigned grid = (unsigned)((n + JAC_ENVS - 1) / JAC_ENVS);
+    CTR_LAUNCH(k_jacobian, kc.mode, dim3(grid), 0, (hipStream_t)stream, kc, joints, sys_idx, n, eps, tip, jac, status);
+    return hip_check("ctr_jacobian launch");
 }
 
 int ctr_set_action(const ctr_env_config_t *cfg, float *joints, const int32_t *sys_idx, const float *actions,

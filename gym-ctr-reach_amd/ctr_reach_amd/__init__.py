@@ -12,3 +12,4 @@ from .vec_env import CtrReachVecEnv  # noqa: F401
 from .env import CtrReachEnv, Model, make  # noqa: F401
 from .systems import Tube, default_kwargs, default_systems_parameters  # noqa: F401
 from .goal_tolerance import GoalTolerance  # noqa: F401
+from .ik import dls_ik_position_only  # noqa: F401

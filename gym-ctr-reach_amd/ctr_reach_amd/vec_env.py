@@ -317,6 +317,20 @@ class CtrReachVecEnv(object):
             return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=stats[:, 2], nseg=stats[:, 3], status=status)
         return tip
 
+    def jacobian(self, joints, system=None, eps=1e-4, stream=None):
+        """Forward-difference tip Jacobian (CTR_Model.jac scheme, CTR_Python/CTR_Model.py:251-262)
+        of this env's FK over float64 joints [M, 6] -> (tip [M, 3], jac [M, 3, 6]) float64 (device)."""
+        torch = _torch()
+        q = torch.as_tensor(joints, dtype=torch.float64, device=self.device).reshape(-1, 6).contiguous()
+        m = q.shape[0]
+        s = None if system is None else torch.as_tensor(system, dtype=torch.int32, device=self.device).reshape(-1).expand(m).contiguous()
+        tip = torch.empty((m, 3), dtype=torch.float64, device=self.device)
+        jac = torch.empty((m, 3, 6), dtype=torch.float64, device=self.device)
+        rc = self.lib.ctr_jacobian(_abi.ptr(q), _abi.ptr(s), m, self.cfg, float(eps), _abi.ptr(tip), _abi.ptr(jac),
+                                   None, _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_jacobian")
+        return tip, jac
+
     def domain_parameters(self, stream=None):
         """Each env's current tube table (Model.current_sys_parameters after randomize_parameters,
         model.py:20-28): dict of [n, 3] float64 device tensors L, L_c, EI, GJ, U_x, U_y,

@@ -25,6 +25,7 @@
  *                       (+ Obs.sample_goal envs/obs.py:185-207, get_obs obs.py:136-164)
  *   ctr_compute_reward  CtrReachEnv.compute_reward(ag, dg, info)          envs/ctr_reach_env.py:160-170
  *   ctr_fk_tables       Model.forward_kinematics with per-row tube tables  envs/model.py:30-70
+ *   ctr_jacobian        CTR_Model.jac (finite differences)             envs/CTR_Python/CTR_Model.py:251-262
  *   ctr_domain_params   Model.current_sys_parameters after randomize_parameters
  *                                                                          envs/model.py:20-28, model_utils.py:5-35
  */
@@ -162,6 +163,14 @@ int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env
  * Model.current_sys_parameters, model.py:13,30).  cfg supplies the integrator and model. */
 int ctr_fk_tables(const float *joints, const ctr_system_t *tables, int64_t n, const ctr_env_config_t *cfg,
                   double *tip, uint32_t *stats, uint32_t *status, void *stream);
+
+/* Forward-difference tip Jacobian d tip / d q over float64 joints [n][6] (device):
+ * jac[n][3][6] = (tip(q + eps e_i) - tip(q)) / eps, the scheme of CTR_Model.jac
+ * (envs/CTR_Python/CTR_Model.py:251-262, eps 1e-4 there) applied to Model.forward_kinematics;
+ * the 7 FKs of an env run on 7 lanes.  tip [n][3] (the unperturbed FK) and status may be NULL;
+ * status bits are OR-ed in. */
+int ctr_jacobian(const double *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg, double eps,
+                 double *tip, double *jac, uint32_t *status, void *stream);
 
 /* n_substeps x Obs.set_action, in place on joints [n][6] (device). */
 int ctr_set_action(const ctr_env_config_t *cfg, float *joints, const int32_t *sys_idx,

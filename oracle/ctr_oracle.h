@@ -40,6 +40,8 @@ void oracle_segments(const float *joints, const int32_t *sys_idx, int64_t n, con
 void oracle_domain_systems(int64_t n, const oracle_system_t *systems, const double *din, const double *dout,
                            const int32_t *sys_idx, double rnd, uint64_t seed, const uint32_t *epoch,
                            int64_t env_base, oracle_system_t *out);
+void oracle_jacobian(const double *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
+                     int integrator, int steps_per_m, int rigid, double eps, double *tip, double *jac);
 int oracle_version(void);
 
 #ifdef __cplusplus

@@ -46,6 +46,7 @@ def lib():
         L.oracle_sample_joints.argtypes = [i64, P, P, u64, P, u32, i64, P, P]
         L.oracle_philox.argtypes = [P, u64]
         L.oracle_segments.argtypes = [P, P, i64, P, P, P]
+        L.oracle_jacobian.argtypes = [P, P, i64, P, ci, ci, ci, ctypes.c_double, P, P]
         L.oracle_domain_systems.argtypes = [i64, P, P, P, P, ctypes.c_double, u64, P, i64, P]
         _lib = L
     return _lib
@@ -122,6 +123,21 @@ def domain_systems(n, rand, seed, epoch, env_base=0, system=None, params=None, s
                                 _p(np.ascontiguousarray(dout)), _p(s), float(rand), int(seed) & (2**64 - 1),
                                 _p(ep), int(env_base), ctypes.cast(out, ctypes.c_void_p))
     return out
+
+
+def jacobian(joints, system=None, systems=None, eps=1e-4, integrator="rk45_scipy", steps_per_m=0,
+             model="compliant"):
+    """Forward-difference tip Jacobian [n, 3, 6] (CTR_Model.jac scheme, CTR_Model.py:251-262) over
+    float64 joints; returns (tip [n, 3], jac)."""
+    it, spm, rg = _fkopts(integrator, steps_per_m, model)
+    q = np.ascontiguousarray(joints, dtype=np.float64).reshape(-1, 6)
+    n = q.shape[0]
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    tip = np.zeros((n, 3)); jac = np.zeros((n, 3, 6))
+    lib().oracle_jacobian(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), it, spm, rg, float(eps), _p(tip),
+                          _p(jac))
+    return tip, jac
 
 
 def fk(joints, system=None, systems=None, integrator="rk45_scipy", steps_per_m=0, model="compliant"):

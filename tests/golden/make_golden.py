@@ -339,11 +339,79 @@ def gen_csv_known(CtrReachEnv, kwargs, rows_per_file):
     print("csv_known", len(J), "reproduced<=1e-12:", int((dev <= 1e-12).sum()), "max dev", dev.max())
 
 
+def gen_jacobian(CtrReachEnv, kwargs, per_sys, eps=1e-4):
+    """Forward-difference tip Jacobian of the reference FK over float64 joints, the scheme of
+    CTR_Model.jac (CTR_Python/CTR_Model.py:251-262) applied to Model.forward_kinematics."""
+    env = make_env(CtrReachEnv, kwargs, select_systems=[0, 1, 2, 3])
+    rng = np.random.default_rng(4321)
+    Q, S, T, JAC = [], [], [], []
+    for s in range(4):
+        L = tube_lengths(kwargs, s)
+        for q32 in sample_valid_joints(rng, L, per_sys):
+            q = q32.astype(np.float64)
+            # keep the perturbed extensions inside the region (b_i + eps <= 0)
+            q[:3] = np.minimum(q[:3], -2 * eps)
+            r0 = np.asarray(env.model.forward_kinematics(q, s), np.float64)
+            jac = np.zeros((3, 6))
+            for i in range(6):
+                qp = q.copy()
+                qp[i] = q[i] + eps
+                jac[:, i] = (np.asarray(env.model.forward_kinematics(qp, s), np.float64) - r0) / eps
+            Q.append(q); S.append(s); T.append(r0); JAC.append(jac)
+    np.savez_compressed(os.path.join(OUT, "jacobian.npz"), joints=np.array(Q), system=np.array(S, np.int32),
+                        tip=np.array(T), jac=np.array(JAC), eps=eps)
+    print("jacobian", len(Q))
+
+
+def gen_backbone(CtrReachEnv, kwargs, per_sys, max_pts=270):
+    """Backbone shape model.r (30 t_eval points per segment, RK45 dense output) with the tube
+    tip indices of ctr_model (model.py:119-174) and the r1/r2/r3 slices (model.py:66-68)."""
+    env = make_env(CtrReachEnv, kwargs, select_systems=[0, 1, 2, 3])
+    model = env.model
+    rng = np.random.default_rng(777)
+    cls_ctr = type(model).ctr_model
+    cap = {}
+
+    def ctr_model(*a, **k):
+        out = cls_ctr(model, *a, **k)
+        cap["tip_idx"] = np.asarray(out[2], np.int64)
+        return out
+
+    Q, S, R, NPT, TIPI, TIP = [], [], [], [], [], []
+    for s in range(4):
+        L = tube_lengths(kwargs, s)
+        qs = list(sample_valid_joints(rng, L, per_sys)) + list(edge_joints(kwargs, s)[:4])
+        for q in qs:
+            model.ctr_model = ctr_model
+            try:
+                tip = model.forward_kinematics(np.asarray(q, np.float32), s)
+            finally:
+                del model.ctr_model
+            r = np.asarray(model.r, np.float64)
+            assert len(r) <= max_pts
+            pad = np.full((max_pts, 3), np.nan)
+            pad[:len(r)] = r
+            Q.append(np.asarray(q, np.float32)); S.append(s); R.append(pad); NPT.append(len(r))
+            TIPI.append(cap["tip_idx"]); TIP.append(np.asarray(tip, np.float64))
+    R = np.array(R)[:, :max(NPT)]
+    np.savez_compressed(os.path.join(OUT, "backbone.npz"), joints=np.array(Q), system=np.array(S, np.int32),
+                        r=R, n_points=np.array(NPT, np.int32), tip_idx=np.array(TIPI, np.int64),
+                        tip=np.array(TIP))
+    print("backbone", len(Q), "max points", max(NPT))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", nargs="*", help="generate only these fixtures (jacobian, backbone)")
     args = ap.parse_args()
     CtrReachEnv, kwargs = load_reference()
+    if args.only:
+        if "jacobian" in args.only:
+            gen_jacobian(CtrReachEnv, kwargs, 4 if args.quick else 32)
+        if "backbone" in args.only:
+            gen_backbone(CtrReachEnv, kwargs, 4 if args.quick else 16)
+        return
     sysj = {}
     for s in range(4):
         p = kwargs["ctr_systems_parameters"]["ctr_%d" % s]
@@ -358,6 +426,8 @@ def main():
     gen_step(CtrReachEnv, kwargs, "step_single.npz", [0], 8 if args.quick else 96)
     gen_step(CtrReachEnv, kwargs, "step_multi.npz", [0, 1, 2, 3], 8 if args.quick else 96)
     gen_csv_known(CtrReachEnv, kwargs, 2 if args.quick else 25)
+    gen_jacobian(CtrReachEnv, kwargs, 4 if args.quick else 32)
+    gen_backbone(CtrReachEnv, kwargs, 4 if args.quick else 16)
 
 
 if __name__ == "__main__":

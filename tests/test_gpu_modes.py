@@ -86,3 +86,14 @@ def test_reset_goals_follow_mode(cuda, oracle_mod):
     dg = oracle_mod.fk(env.desired_joints.cpu().numpy(), sysid, integrator="rk4", steps_per_m=100,
                        model="rigid")["tip"]
     assert np.abs(env.desired_goal.cpu().numpy() - dg).max() < 1e-11
+
+
+def test_tube_gap_nan_status(cuda):
+    """A tube gap (joints outside the nesting constraints) gives a NaN tip and CTR_STATUS_NAN
+    (the reference never returns there; see test_oracle_modes.py)."""
+    from ctr_reach_amd import CtrReachVecEnv
+    from test_oracle_modes import GAP_JOINTS
+    env = CtrReachVecEnv(1, device=cuda)
+    tip, st = env.forward_kinematics(np.array([GAP_JOINTS], np.float32), return_stats=True)
+    assert np.isnan(tip.cpu().numpy()).all()
+    assert st["status"].cpu().numpy()[0] & 4

@@ -73,3 +73,26 @@ def test_domain_draws_distribution(oracle_mod):
         assert all(getattr(ds[i], field)[2] == getattr(nom, field)[2] for i in range(0, n, 97))
     d0 = oracle_mod.domain_systems(4, r, seed=5, epoch=0)
     assert all(d0[i].E[0] == nom.E[0] and d0[i].I[0] == nom.I[0] for i in range(4))
+
+
+def test_jacobian_vs_reference(golden_dir, oracle_mod):
+    """Forward-difference Jacobian over float64 joints vs the reference FK's own differences
+    (tests/golden/jacobian.npz, make_golden.py gen_jacobian).  The 1/eps = 1e4 amplification of
+    ~1e-15 m tip rounding gives ~1e-11."""
+    d = _d(golden_dir, "jacobian.npz")
+    tip, jac = oracle_mod.jacobian(d["joints"], d["system"], eps=float(d["eps"]))
+    assert np.abs(tip - d["tip"]).max() < 1e-12
+    assert np.abs(jac - d["jac"]).max() < 1e-9
+
+
+GAP_JOINTS = [-0.4048666928673197, -0.33618654488386224, 0.03616300441854741, -2.1221680754721732,
+              -1.6713142619158792, 1.7601462221235273]
+
+
+def test_tube_gap_gives_nan_not_a_hang(oracle_mod):
+    """Joints outside the nesting constraints can leave an arclength gap with no tube.  The
+    reference's RHS is NaN there and scipy's step loop never terminates (checked by hand: the
+    unmodified reference FK does not return on these joints).  The oracle and the kernels stop
+    with a NaN tip and CTR_STATUS_NAN."""
+    r = oracle_mod.fk(np.array([GAP_JOINTS], np.float32))
+    assert np.isnan(r["tip"]).all() and r["status"][0] & 4
