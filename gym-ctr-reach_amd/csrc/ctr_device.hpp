@@ -255,7 +255,46 @@ constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 
                  E5 = -22.0 / 525, E6 = 1.0 / 40;
 constexpr double RTOL = 1e-3, ATOL = 1e-6;
 constexpr double INV_SQRT18 = 0.23570226039551584;
+// dense-output matrix P (scipy rk.py RK45.P), rows = stages 0..6, columns = powers x^1..x^4
+constexpr double P0[4] = {1.0, -8048581381.0 / 2820520608, 8663915743.0 / 2820520608, -12715105075.0 / 11282082432};
+constexpr double P1[4] = {0.0, 0.0, 0.0, 0.0};
+constexpr double P2[4] = {0.0, 131558114200.0 / 32700410799, -68118460800.0 / 10900136933,
+                          87487479700.0 / 32700410799};
+constexpr double P3[4] = {0.0, -1754552775.0 / 470086768, 14199869525.0 / 1410260304, -10690763975.0 / 1880347072};
+constexpr double P4[4] = {0.0, 127303824393.0 / 49829197408, -318862633887.0 / 49829197408,
+                          701980252875.0 / 199316789632};
+constexpr double P5[4] = {0.0, -282668133.0 / 205662961, 2019193451.0 / 616988883, -1453857185.0 / 822651844};
+constexpr double P6[4] = {0.0, 40617522.0 / 29380423, -110615467.0 / 29380423, 69997945.0 / 29380423};
+constexpr int SHAPE_PTS = 30;          // t_eval points per segment (model.py:141 linspace num=30)
 }  // namespace rk
+
+// Backbone-shape output of one lane (model.py:66-68,141-164): r at the 30 sorted linspace
+// points of every integrated segment (RK45 dense output, scipy rk.py RkDenseOutput), and the
+// arclength of each point (ctr_model's Length).  Points beyond `cap` are counted, not stored.
+struct ShapeOut {
+    double *r;        // [cap][3]
+    double *s;        // [cap]
+    int cap;
+    int count;
+};
+
+// numpy.linspace(a, b, 30) element i (numpy 2: i * step + a, step = (b - a) / 29; last = b),
+// without contraction.
+__device__ __forceinline__ double linspace30(double a, double b, double step, int i)
+{
+    return i == rk::SHAPE_PTS - 1 ? b : __dadd_rn(__dmul_rn((double)i, step), a);
+}
+
+__device__ __forceinline__ void shape_put(ShapeOut *so, double s, const double r[3])
+{
+    if (so->count < so->cap) {
+        so->s[so->count] = s;
+        so->r[3 * so->count + 0] = r[0];
+        so->r[3 * so->count + 1] = r[1];
+        so->r[3 * so->count + 2] = r[2];
+    }
+    so->count++;
+}
 
 struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
@@ -293,8 +332,8 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
 // Forward kinematics of one lane, scipy-RK45 integrator: joints (f64; the env's float32 joints
 // promoted exactly as model.py:51 does) -> tip (f64).  RIGID: torsionally rigid variant (GJ -> inf:
 // u_z stays 0, the tube angles stay at their joint values, so the trig is computed once).
-template <bool HAS_UY, bool RIGID>
-__device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st)
+template <bool HAS_UY, bool RIGID, bool SHAPE = false>
+__device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st, ShapeOut *so = nullptr)
 {
     using namespace rk;
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};
@@ -320,6 +359,9 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
     double t = 0.0, tb = 0.0, ha = 0.0, min_step = 0.0, prev_end = 0.0;
     uint32_t remaining = sg.kept;   // kept gaps not yet integrated, in arclength order
     bool need_init = true, new_step = true, rejected = false;
+    double sh_a = 0.0, sh_b = 0.0, sh_step = 0.0;   // SHAPE: the segment's t_eval linspace
+    bool sh_rev = false;
+    int sh_j = 0;                                   // SHAPE: next t_eval point of the segment
 
 #ifdef CTR_DIAG_TIME
     uint64_t c_init = 0, c_stage = 0, c_tail = 0;
@@ -343,6 +385,14 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             const double t0 = fmin(a, b);
             tb = fmax(a, b);                                      // :145-151 sorted span
             prev_end = endk;
+            if (SHAPE) {
+                // t_eval = sorted(linspace(a, b, 30)) (model.py:141-147)
+                sh_a = a;
+                sh_b = b;
+                sh_step = (b - a) / 29.0;
+                sh_rev = a > b;
+                sh_j = 0;
+            }
             // RungeKutta.__init__: f = fun(t0, y0) -- the trig of y is already known
             rhs_core<HAS_UY>(p, ty, yu, yR, f.uz, f.R);
             double fr[3];
@@ -352,7 +402,12 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             st.nseg++;
 #endif
             const double interval = tb - t0;
-            if (interval == 0.0) continue;                        // OdeSolver.step: t == t_bound
+            if (interval == 0.0) {                                // OdeSolver.step: t == t_bound
+                if (SHAPE)                                        // ConstantDenseOutput(y)
+                    for (int j = 0; j < SHAPE_PTS; ++j)
+                        shape_put(so, linspace30(sh_a, sh_b, sh_step, sh_rev ? SHAPE_PTS - 1 - j : j), yr);
+                continue;
+            }
             if (p.present == 0u) {
                 // a gap with no tube (joints outside the nesting constraints): the reference's
                 // RHS is NaN (1/sum EI = inf, model.py:87-93) and scipy's step loop never ends
@@ -447,6 +502,12 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         double br[3], er[3];
         #pragma unroll
         for (int i = 0; i < 3; ++i) { br[i] = fr[i] * B0; er[i] = fr[i] * E0; }
+        double qr[3][4];                             // SHAPE: Q = K^T P for the r components
+        if (SHAPE)
+            #pragma unroll
+            for (int i = 0; i < 3; ++i)
+                #pragma unroll
+                for (int j = 0; j < 4; ++j) qr[i][j] = fr[i] * P0[j];
 
         Stage K1, K2, K3, K4, K5;
         double ui[3], ai[3], Ri[9], rc[3];
@@ -456,7 +517,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         const double a30 = A30 * h, a31 = A31 * h, a32 = A32 * h;
         const double a40 = A40 * h, a41 = A41 * h, a42 = A42 * h, a43 = A43 * h;
         const double a50 = A50 * h, a51 = A51 * h, a52 = A52 * h, a53 = A53 * h, a54 = A54 * h;
-#define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF)                                  \
+#define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF, PROW)                            \
         {                                                                                      \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
                 ui[i] = EXPR_U;                                                                \
@@ -470,22 +531,25 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
                 br[i] += rc[i] * (BCOEF);                                                      \
                 er[i] += rc[i] * (ECOEF);                                                      \
             }                                                                                  \
+            if (SHAPE)                                                                         \
+                _Pragma("unroll") for (int i = 0; i < 3; ++i)                                  \
+                    _Pragma("unroll") for (int j = 0; j < 4; ++j) qr[i][j] += rc[i] * PROW[j]; \
         }
         CTR_STAGE(K1, fma(f.uz[i], a10, yu[i]),
                   fma(f.al[i], a10, ya[i]),
-                  fma(f.R[i], a10, yR[i]), 0.0, 0.0)
+                  fma(f.R[i], a10, yR[i]), 0.0, 0.0, P1)
         CTR_STAGE(K2, fma(K1.uz[i], a21, fma(f.uz[i], a20, yu[i])),
                   fma(K1.al[i], a21, fma(f.al[i], a20, ya[i])),
-                  fma(K1.R[i], a21, fma(f.R[i], a20, yR[i])), B2, E2)
+                  fma(K1.R[i], a21, fma(f.R[i], a20, yR[i])), B2, E2, P2)
         CTR_STAGE(K3, fma(K2.uz[i], a32, fma(K1.uz[i], a31, fma(f.uz[i], a30, yu[i]))),
                   fma(K2.al[i], a32, fma(K1.al[i], a31, fma(f.al[i], a30, ya[i]))),
-                  fma(K2.R[i], a32, fma(K1.R[i], a31, fma(f.R[i], a30, yR[i]))), B3, E3)
+                  fma(K2.R[i], a32, fma(K1.R[i], a31, fma(f.R[i], a30, yR[i]))), B3, E3, P3)
         CTR_STAGE(K4, fma(K3.uz[i], a43, fma(K2.uz[i], a42, fma(K1.uz[i], a41, fma(f.uz[i], a40, yu[i])))),
                   fma(K3.al[i], a43, fma(K2.al[i], a42, fma(K1.al[i], a41, fma(f.al[i], a40, ya[i])))),
-                  fma(K3.R[i], a43, fma(K2.R[i], a42, fma(K1.R[i], a41, fma(f.R[i], a40, yR[i])))), B4, E4)
+                  fma(K3.R[i], a43, fma(K2.R[i], a42, fma(K1.R[i], a41, fma(f.R[i], a40, yR[i])))), B4, E4, P4)
         CTR_STAGE(K5, fma(K4.uz[i], a54, fma(K3.uz[i], a53, fma(K2.uz[i], a52, fma(K1.uz[i], a51, fma(f.uz[i], a50, yu[i]))))),
                   fma(K4.al[i], a54, fma(K3.al[i], a53, fma(K2.al[i], a52, fma(K1.al[i], a51, fma(f.al[i], a50, ya[i]))))),
-                  fma(K4.R[i], a54, fma(K3.R[i], a53, fma(K2.R[i], a52, fma(K1.R[i], a51, fma(f.R[i], a50, yR[i]))))), B5, E5)
+                  fma(K4.R[i], a54, fma(K3.R[i], a53, fma(K2.R[i], a52, fma(K1.R[i], a51, fma(f.R[i], a50, yR[i]))))), B5, E5, P5)
 #undef CTR_STAGE
         CTR_STAMP(ts2);
         // y_new (rk.py rk_step) and the error sums without K6
@@ -539,6 +603,26 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
             ha *= factor;
+            if (SHAPE) {
+                // ivp.py t_eval: the points in (t_old, t_new] (and t0 itself on the first step)
+                // from this step's dense output y_old + h Q [x, x^2, x^3, x^4], x = (s - t_old)/h
+                #pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    #pragma unroll
+                    for (int j = 0; j < 4; ++j) qr[i][j] += k6r[i] * P6[j];
+                while (sh_j < SHAPE_PTS) {
+                    const double te = linspace30(sh_a, sh_b, sh_step, sh_rev ? SHAPE_PTS - 1 - sh_j : sh_j);
+                    if (te > tnew) break;
+                    const double x = (te - t) / h;
+                    const double x2 = x * x, x3 = x2 * x, x4 = x3 * x;
+                    double rp[3];
+                    #pragma unroll
+                    for (int i = 0; i < 3; ++i)
+                        rp[i] = h * (qr[i][0] * x + qr[i][1] * x2 + qr[i][2] * x3 + qr[i][3] * x4) + yr[i];
+                    shape_put(so, te, rp);
+                    ++sh_j;
+                }
+            }
             #pragma unroll
             for (int i = 0; i < 3; ++i) { yu[i] = nu[i]; ya[i] = na[i]; yr[i] = nr[i]; }
             #pragma unroll

@@ -10,6 +10,7 @@
 //                 for the queued / masked envs                        (envs/ctr_reach_env.py:70-114)
 //   k_refill      precomputes queued resets into the pool, two lanes per reset
 //   k_reward      compute_reward over a batch                          (envs/ctr_reach_env.py:160-170)
+//   k_fk_shape    FK + backbone shape r at 30 dense-output points/segment (envs/model.py:66-68,119-174)
 //   k_jacobian    forward-difference tip Jacobian, 7 lanes per env       (CTR_Python/CTR_Model.py:251-262)
 //   k_domain_params  each env's current (domain-randomised) tube table  (envs/model.py:20-28)
 //
@@ -187,6 +188,44 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
     if (status) status[e] = st.status;
 }
 
+
+// Backbone shape (model.py:66-68, 119-174): the FK plus r at the 30 t_eval points of every
+// segment from the RK45 dense output.  Row e writes r[e][cap][3], s[e][cap], npts[e].
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_fk_shape(KCfg kc, const float *__restrict__ joints,
+                                                       const int32_t *__restrict__ sys_idx,
+                                                       const ctr_system_t *__restrict__ tables, int64_t n, int32_t cap,
+                                                       double *__restrict__ tip, double *__restrict__ r,
+                                                       double *__restrict__ s_out, int32_t *__restrict__ npts,
+                                                       uint32_t *__restrict__ status)
+{
+    if constexpr ((MODE & 2) == 0) {          // RK45 only (the host rejects RK4)
+        __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
+        stage_systems(kc, s_sys);
+        const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+        if (e >= n) return;
+        double q[6];
+        #pragma unroll
+        for (int i = 0; i < 6; ++i) q[i] = (double)joints[6 * e + i];
+        const int s = sys_idx ? clamp_sys(sys_idx[e], kc.c.n_systems) : 0;
+        const SysK *sy = &s_sys[s];
+        if (tables) {
+            SysK &me = s_lane_dyn[threadIdx.x];
+            static_cast<ctr_system_t &>(me) = tables[e];
+            #pragma unroll
+            for (int j = 0; j < 11; ++j) sysk_derive(me, j);
+            sy = &me;
+        }
+        FkStats st = {0, 0, 0, 0, 0};
+        ShapeOut so = {r + (int64_t)3 * cap * e, s_out + (int64_t)cap * e, cap, 0};
+        double out[3];
+        fk_lane<(MODE & 1) != 0, (MODE & 4) != 0, true>(*sy, q, out, st, &so);
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) tip[3 * e + i] = out[i];
+        npts[e] = so.count;
+        if (status) status[e] = st.status;
+    }
+}
 
 // Forward-difference tip Jacobian, SEVEN lanes per environment: lane c < 6 integrates the FK at
 // q + eps e_c, lane 6 at q (CTR_Model.jac, CTR_Python/CTR_Model.py:251-262, applied to this
@@ -647,6 +686,23 @@ int ctr_fk_tables(const float *joints, const ctr_system_t *tables, int64_t n, co
 {
     if (n > 0 && !tables) return fail(CTR_EINVAL, "ctr_fk_tables: tables is NULL");
     return fk_impl(joints, nullptr, tables, n, cfg, tip, stats, status, stream);
+}
+
+int ctr_fk_shape(const float *joints, const int32_t *sys_idx, const ctr_system_t *tables, int64_t n,
+                 const ctr_env_config_t *cfg, int32_t cap, double *tip, double *r, double *s, int32_t *npts,
+                 uint32_t *status, void *stream)
+{
+    if (int rc = check_cfg(cfg)) return rc;
+    if (cfg->integrator != CTR_INTEGRATOR_RK45_SCIPY)
+        return fail(CTR_EINVAL, "ctr_fk_shape: the backbone dense output needs integrator rk45_scipy");
+    if (n < 0 || cap < 0 || (n > 0 && (!joints || !tip || !npts || (cap > 0 && (!r || !s)))))
+        return fail(CTR_EINVAL, "ctr_fk_shape: bad buffers");
+    if (n == 0) return 0;
+    KCfg kc = make_kcfg(cfg);
+    if (tables) kc.mode |= 1;
+    CTR_LAUNCH(k_fk_shape, kc.mode, dim3(grid_for(n)), tables ? (size_t)BLOCK * sizeof(SysK) : 0, (hipStream_t)stream,
+               kc, joints, sys_idx, tables, n, cap, tip, r, s, npts, status);
+    return hip_check("ctr_fk_shape launch");
 }
 
 int ctr_jacobian(const double *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg, double eps,

@@ -98,7 +98,7 @@ class CtrStepOut(ctypes.Structure):
 
 
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
-            "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian")
+            "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape")
 
 _lib = None
 
@@ -128,9 +128,10 @@ def load(path=None):
     L.ctr_compute_reward.argtypes = [_P, _P, i64, ctypes.c_double, _P, _P]
     L.ctr_domain_params.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P]
     L.ctr_fk_tables.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), _P, _P, _P, _P]
+    L.ctr_fk_shape.argtypes = [_P, _P, _P, i64, ctypes.POINTER(CtrEnvConfig), i32, _P, _P, _P, _P, _P, _P]
     L.ctr_jacobian.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), ctypes.c_double, _P, _P, _P, _P]
     for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward",
-               "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian"):
+               "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape"):
         getattr(L, fn).restype = ctypes.c_int
     if L.ctr_abi_version() != CTR_ABI_VERSION:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))

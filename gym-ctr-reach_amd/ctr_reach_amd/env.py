@@ -13,20 +13,76 @@ from .systems import default_kwargs
 from .vec_env import CtrReachVecEnv
 
 
+def tube_tip_indices(s, L, beta):
+    """ctr_model's tip_pos (model.py:160-168): for each tube k the first backbone index whose
+    arclength is >= L_k + beta_k - 1e-3 (0 if none)."""
+    s = np.asarray(s)
+    out = np.zeros(3, np.int64)
+    for k in range(3):
+        hit = np.nonzero(s >= (float(L[k]) + float(beta[k])) - 1e-3)[0]
+        out[k] = hit[0] if hit.size else 0
+    return out
+
+
 class Model(object):
-    """Operator boundary: Model.forward_kinematics (envs/model.py:30-70), batched on the GPU."""
+    """Operator boundary: Model.forward_kinematics (envs/model.py:30-70), batched on the GPU.
+
+    ``r``, ``r1``, ``r2``, ``r3`` are the backbone of the last forward kinematics (model.py:66-68):
+    a one-row call computes them with ctr_fk_shape; after env.reset()/step() they are computed
+    on first access for the env's current joints (the reference's last FK in both)."""
 
     def __init__(self, vec_env):
         self._env = vec_env
-        self.r = self.r1 = self.r2 = self.r3 = None   # backbone shape: not produced (render is out of scope)
+        self._shape = None        # (r, r1, r2, r3)
+        self._pending = None      # (joints, system) whose shape is computed on first access
+
+    def _tables(self, system, m):
+        v = self._env
+        if v.kwargs.get("domain_rand", 0.0) != 0.0 and int(system) == int(v.system[0].item()):
+            # the episode's randomised table (Model.current_sys_parameters, model.py:20-28)
+            return v.domain_parameters()["table"][0:1].expand(m, 18)
+        return None
+
+    def _compute_shape(self, q, system):
+        v = self._env
+        tb = self._tables(system, 1)
+        out = v.forward_kinematics_shape(q.reshape(1, 6), None if tb is not None else np.array([int(system)]),
+                                         tables=tb)
+        n = int(out["npts"][0].item())
+        r = out["r"][0, :n].cpu().numpy()
+        s = out["s"][0, :n].cpu().numpy()
+        L = v.domain_parameters()["L"][0].cpu().numpy() if tb is not None else \
+            [t.L for t in v.ctr_system_parameters[int(system)]]
+        beta = q.reshape(6)[:3].astype(np.float64)
+        t0, t1, t2 = tube_tip_indices(s, L, beta)
+        return out["tip"][0].cpu().numpy(), (r, r[t1:t0 + 1], r[t2:t1 + 1], r[:t2 + 1])
+
+    def _set_pending(self, joints, system):
+        self._pending = (np.asarray(joints, np.float32).copy(), int(system))
+        self._shape = None
+
+    def _current_shape(self):
+        if self._shape is None and self._pending is not None:
+            q, s = self._pending
+            self._shape = self._compute_shape(q, s)[1]
+        return self._shape if self._shape is not None else (None, None, None, None)
+
+    r = property(lambda self: self._current_shape()[0])
+    r1 = property(lambda self: self._current_shape()[1])
+    r2 = property(lambda self: self._current_shape()[2])
+    r3 = property(lambda self: self._current_shape()[3])
 
     def forward_kinematics(self, joint, system, **kwargs):
         q = np.asarray(joint, dtype=np.float32).reshape(-1, 6)
         v = self._env
-        if v.kwargs.get("domain_rand", 0.0) != 0.0 and int(system) == int(v.system[0].item()):
-            # the episode's randomised table (Model.current_sys_parameters, model.py:20-28)
-            table = v.domain_parameters()["table"][0:1].expand(q.shape[0], 18)
-            tip = v.forward_kinematics(q, tables=table)
+        if q.shape[0] == 1 and v.integrator == "rk45_scipy":
+            tip, self._shape = self._compute_shape(q, system)
+            self._pending = None
+            assert not np.any(np.isnan(self._shape[0]))          # model.py:69
+            return tip if np.ndim(joint) == 1 else tip[None]
+        tb = self._tables(system, q.shape[0])
+        if tb is not None:
+            tip = v.forward_kinematics(q, tables=tb)
         else:
             tip = v.forward_kinematics(q, np.full(q.shape[0], int(system)))
         out = tip.cpu().numpy()
@@ -94,6 +150,7 @@ class CtrReachEnv(GoalEnvBase):
         self.starting_joints = self.vec.joints[0].cpu().numpy().copy()
         if self.vec.desired_joints is not None and goal is None:
             self.desired_joints = self.vec.desired_joints[0].cpu().numpy().copy()
+        self.model._set_pending(self.starting_joints, self.system)
         return self._obs()
 
     def _obs(self):
@@ -112,6 +169,7 @@ class CtrReachEnv(GoalEnvBase):
         a = torch.as_tensor(np.asarray(action, np.float32).reshape(1, 6), device=self.vec.device)
         obs, reward, done, info = self.vec.step(a)
         self.t = int(self.vec.t[0].item())
+        self.model._set_pending(self.vec.joints[0].cpu().numpy(), self.system)
         o = self._obs()
         achieved_goal = o["achieved_goal"]
         reward = float(reward[0].item())

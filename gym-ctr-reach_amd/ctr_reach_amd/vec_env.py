@@ -317,6 +317,27 @@ class CtrReachVecEnv(object):
             return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=stats[:, 2], nseg=stats[:, 3], status=status)
         return tip
 
+    def forward_kinematics_shape(self, joints, system=None, tables=None, stream=None, cap=270):
+        """Model.forward_kinematics with the backbone shape (model.py:66-68, 119-174) for joints
+        [M, 6]: dict of device tensors tip [M, 3], r [M, cap, 3] and s [M, cap] (valid up to
+        npts [M] = 30 x segments; the rest is NaN), status [M]."""
+        torch = _torch()
+        q = torch.as_tensor(joints, dtype=torch.float32, device=self.device).reshape(-1, 6).contiguous()
+        m = q.shape[0]
+        s = None if system is None else torch.as_tensor(system, dtype=torch.int32, device=self.device).reshape(-1).expand(m).contiguous()
+        tb = None
+        if tables is not None:
+            tb = torch.as_tensor(tables, dtype=torch.float64, device=self.device).reshape(m, 18).contiguous()
+        tip = torch.empty((m, 3), dtype=torch.float64, device=self.device)
+        r = torch.full((m, cap, 3), float("nan"), dtype=torch.float64, device=self.device)
+        sv = torch.full((m, cap), float("nan"), dtype=torch.float64, device=self.device)
+        npts = torch.zeros(m, dtype=torch.int32, device=self.device)
+        status = torch.zeros(m, dtype=torch.int32, device=self.device)
+        rc = self.lib.ctr_fk_shape(_abi.ptr(q), _abi.ptr(s), _abi.ptr(tb), m, self.cfg, int(cap), _abi.ptr(tip),
+                                   _abi.ptr(r), _abi.ptr(sv), _abi.ptr(npts), _abi.ptr(status), _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_fk_shape")
+        return dict(tip=tip, r=r, s=sv, npts=npts, status=status)
+
     def jacobian(self, joints, system=None, eps=1e-4, stream=None):
         """Forward-difference tip Jacobian (CTR_Model.jac scheme, CTR_Python/CTR_Model.py:251-262)
         of this env's FK over float64 joints [M, 6] -> (tip [M, 3], jac [M, 3, 6]) float64 (device)."""

@@ -25,6 +25,7 @@
  *                       (+ Obs.sample_goal envs/obs.py:185-207, get_obs obs.py:136-164)
  *   ctr_compute_reward  CtrReachEnv.compute_reward(ag, dg, info)          envs/ctr_reach_env.py:160-170
  *   ctr_fk_tables       Model.forward_kinematics with per-row tube tables  envs/model.py:30-70
+ *   ctr_fk_shape        Model.forward_kinematics + Model.r / r1 / r2 / r3  envs/model.py:30-70,119-174
  *   ctr_jacobian        CTR_Model.jac (finite differences)             envs/CTR_Python/CTR_Model.py:251-262
  *   ctr_domain_params   Model.current_sys_parameters after randomize_parameters
  *                                                                          envs/model.py:20-28, model_utils.py:5-35
@@ -163,6 +164,16 @@ int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env
  * Model.current_sys_parameters, model.py:13,30).  cfg supplies the integrator and model. */
 int ctr_fk_tables(const float *joints, const ctr_system_t *tables, int64_t n, const ctr_env_config_t *cfg,
                   double *tip, uint32_t *stats, uint32_t *status, void *stream);
+
+/* Model.forward_kinematics with the backbone shape (Model.r, model.py:66-68 and ctr_model
+ * model.py:119-174): besides the tip, r at the 30 sorted linspace points of every segment
+ * (solve_ivp t_eval, RK45 dense output) and their arclengths s (ctr_model's Length), row-major
+ * r [n][cap][3], s [n][cap]; npts [n] = 30 x segments (points past cap are not stored).
+ * cap = 270 always suffices (<= 9 segments).  tables [n] or NULL: per-row tube tables as in
+ * ctr_fk_tables (sys_idx is then ignored).  Needs integrator rk45_scipy.  (device) */
+int ctr_fk_shape(const float *joints, const int32_t *sys_idx, const ctr_system_t *tables, int64_t n,
+                 const ctr_env_config_t *cfg, int32_t cap, double *tip, double *r, double *s, int32_t *npts,
+                 uint32_t *status, void *stream);
 
 /* Forward-difference tip Jacobian d tip / d q over float64 joints [n][6] (device):
  * jac[n][3][6] = (tip(q + eps e_i) - tip(q)) / eps, the scheme of CTR_Model.jac

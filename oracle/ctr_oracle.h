@@ -42,6 +42,8 @@ void oracle_domain_systems(int64_t n, const oracle_system_t *systems, const doub
                            int64_t env_base, oracle_system_t *out);
 void oracle_jacobian(const double *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
                      int integrator, int steps_per_m, int rigid, double eps, double *tip, double *jac);
+void oracle_fk_shape(const float *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
+                     int cap, double *tip, double *r, double *s, int32_t *npts, int32_t *status);
 int oracle_version(void);
 
 #ifdef __cplusplus

@@ -47,6 +47,7 @@ def lib():
         L.oracle_philox.argtypes = [P, u64]
         L.oracle_segments.argtypes = [P, P, i64, P, P, P]
         L.oracle_jacobian.argtypes = [P, P, i64, P, ci, ci, ci, ctypes.c_double, P, P]
+        L.oracle_fk_shape.argtypes = [P, P, i64, P, ci, P, P, P, P, P]
         L.oracle_domain_systems.argtypes = [i64, P, P, P, P, ctypes.c_double, u64, P, i64, P]
         _lib = L
     return _lib
@@ -122,6 +123,30 @@ def domain_systems(n, rand, seed, epoch, env_base=0, system=None, params=None, s
     lib().oracle_domain_systems(n, ctypes.cast(systems, ctypes.c_void_p), _p(np.ascontiguousarray(din)),
                                 _p(np.ascontiguousarray(dout)), _p(s), float(rand), int(seed) & (2**64 - 1),
                                 _p(ep), int(env_base), ctypes.cast(out, ctypes.c_void_p))
+    return out
+
+
+def fk_shape(joints, system=None, systems=None, cap=270):
+    """Model.forward_kinematics with Model.r (model.py:66-68, 119-174): dict tip [n, 3],
+    r [n, cap, 3] and s [n, cap] (NaN past npts), npts [n], status [n]."""
+    q = np.ascontiguousarray(joints, dtype=np.float32).reshape(-1, 6)
+    n = q.shape[0]
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    tip = np.zeros((n, 3)); r = np.full((n, cap, 3), np.nan); sv = np.full((n, cap), np.nan)
+    npts = np.zeros(n, np.int32); status = np.zeros(n, np.int32)
+    lib().oracle_fk_shape(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), int(cap), _p(tip), _p(r), _p(sv),
+                          _p(npts), _p(status))
+    return dict(tip=tip, r=r, s=sv, npts=npts, status=status)
+
+
+def tube_tip_indices(s, L, beta):
+    """ctr_model's tip_pos (model.py:160-168): first index with Length >= L_k + beta_k - 1e-3
+    (0 if none), for k = 0, 1, 2."""
+    out = np.zeros(3, np.int64)
+    for k in range(3):
+        hit = np.nonzero(s >= (L[k] + beta[k]) - 1e-3)[0]
+        out[k] = hit[0] if hit.size else 0
     return out
 
 

@@ -96,3 +96,19 @@ def test_tube_gap_gives_nan_not_a_hang(oracle_mod):
     with a NaN tip and CTR_STATUS_NAN."""
     r = oracle_mod.fk(np.array([GAP_JOINTS], np.float32))
     assert np.isnan(r["tip"]).all() and r["status"][0] & 4
+
+
+def test_backbone_shape_vs_reference(golden_dir, oracle_mod):
+    """Model.r (30 dense-output points per segment) and ctr_model's tube tip indices against the
+    reference (tests/golden/backbone.npz)."""
+    d = _d(golden_dir, "backbone.npz")
+    o = oracle_mod.fk_shape(d["joints"], d["system"])
+    np.testing.assert_array_equal(o["npts"], d["n_points"])
+    P = d["r"].shape[1]
+    assert np.nanmax(np.abs(o["r"][:, :P] - d["r"])) < 1e-13
+    sy = oracle_mod.make_systems()
+    for i in range(len(d["joints"])):
+        s = d["system"][i]
+        L = [sy[s].L[k] for k in range(3)]
+        ti = oracle_mod.tube_tip_indices(o["s"][i, :o["npts"][i]], L, d["joints"][i, :3].astype(np.float64))
+        np.testing.assert_array_equal(ti, d["tip_idx"][i])
