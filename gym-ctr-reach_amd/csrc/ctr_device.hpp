@@ -310,6 +310,14 @@ __device__ __forceinline__ uint64_t stamp()
     return t;
 }
 #define CTR_STAMP(var) const uint64_t var = stamp()
+#elif defined(CTR_ASM_MARKERS)
+// asm-listing build: a comment + scheduling barrier at each block boundary (instruction counts)
+#define CTR_STAMP(var)                                   \
+    do {                                                 \
+        __builtin_amdgcn_sched_barrier(0);               \
+        asm volatile(";CTR_MARK " #var ::: "memory");    \
+        __builtin_amdgcn_sched_barrier(0);               \
+    } while (0)
 #else
 #define CTR_STAMP(var)
 #endif
@@ -328,6 +336,7 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
     for (int j = 0; j < 3; ++j) k.al[j] = ((p.present >> j) & 1u) ? uz[j] : 0.0;
     rcol[0] = R[2]; rcol[1] = R[5]; rcol[2] = R[8];
 }
+
 
 // Forward kinematics of one lane, scipy-RK45 integrator: joints (f64; the env's float32 joints
 // promoted exactly as model.py:51 does) -> tip (f64).  RIGID: torsionally rigid variant (GJ -> inf:

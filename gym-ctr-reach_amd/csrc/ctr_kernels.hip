@@ -640,6 +640,14 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
 // Launch kernel template K<MODE> for the runtime mode (8 instantiations).
+#ifdef CTR_AB_MODE0
+// A/B experiment builds: mode 0 only (system-0 headline workload), 8x faster to compile
+#define CTR_LAUNCH(K, MODE, GRID, SHM, STREAM, ...)                                                \
+    do {                                                                                           \
+        if ((MODE) != 0) return fail(CTR_EINVAL, "A/B build: mode 0 only");                      \
+        hipLaunchKernelGGL(K<0>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__);                     \
+    } while (0)
+#else
 #define CTR_LAUNCH(K, MODE, GRID, SHM, STREAM, ...)                                                     \
     do {                                                                                           \
         switch (MODE) {                                                                            \
@@ -653,6 +661,7 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK)
         default: hipLaunchKernelGGL(K<7>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;       \
         }                                                                                          \
     } while (0)
+#endif
 
 }  // namespace
 

@@ -16,4 +16,6 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_
     python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc3.log 2>&1 || exit 4
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/pmc_f64 -o run -- \
     python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc4.log 2>&1 || echo "pmc4 failed (counter names?)"
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS --output-format csv -d $OUT/pmc_mix -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc5.log 2>&1 || echo "pmc5 failed (counter names?)"
 find $OUT -name "*.csv" | head -50
