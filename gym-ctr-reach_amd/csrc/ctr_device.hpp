@@ -177,14 +177,32 @@ struct Trig {
     double c10, s10, c20, s20, c21, s21;   // cos/sin(alpha_i - alpha_j)
 };
 
+#ifndef CTR_TRIG_POLY
+// (sin, cos)(k pi/32) table for sincos_tab, one copy per workgroup in LDS; every kernel that
+// integrates calls trig_table_fill() before its first barrier.
+__shared__ double s_trig_tab[64][2];
+
+__device__ __forceinline__ void trig_table_fill()
+{
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
+}
+#else
+__device__ __forceinline__ void trig_table_fill() {}
+#endif
+
 __device__ __forceinline__ Trig trig_of(const double al[3])
 {
     Trig t;
     const double d10 = al[1] - al[0], d20 = al[2] - al[0];
     // both reductions branch-free and interleavable; the exact slow path only when some lane
     // of the wave has a huge / non-finite angle (wave-uniform branch)
+#ifndef CTR_TRIG_POLY
+    ctr_math::sincos_tab(d10, s_trig_tab, t.s10, t.c10);
+    ctr_math::sincos_tab(d20, s_trig_tab, t.s20, t.c20);
+#else
     ctr_math::sincos_fast(d10, t.s10, t.c10);
     ctr_math::sincos_fast(d20, t.s20, t.c20);
+#endif
     if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10) || ctr_math::sincos_needs_slow(d20)) != 0, 0)) {
         if (ctr_math::sincos_needs_slow(d10)) {
             const ctr_math::SinCos r = ctr_math::sincos_slow(d10);

@@ -64,6 +64,7 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tub
     const int nd = kc.c.n_systems * ND;
     for (int i = threadIdx.x; i < nd; i += blockDim.x)
         reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND]))[i % ND] = src[i];
+    trig_table_fill();
     if (raw_lds) {
         constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
         const double *rs = reinterpret_cast<const double *>(kc.c.raw);

@@ -42,6 +42,7 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
     r = fma(-n, 6.123233995736766e-17, r);
     r = fma(-n, -1.4973849048591698e-33, r);
     const double z = r * r;
+#ifdef CTR_SINCOS_HORNER
     // sin kernel (|r| <= pi/4)
     const double ps = 8.33333333332248946124e-03 +
                       z * (-1.98412698298579493134e-04 +
@@ -54,6 +55,19 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
                                 z * (2.48015872894767294178e-05 +
                                      z * (-2.75573143513906633035e-07 +
                                           z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+#else
+    // Estrin evaluation of the same minimax kernels: dependency depth 3 instead of 5-6 (one
+    // wave per SIMD exposes fp64 FMA latency)
+    const double z2 = z * z;
+    const double sa = fma(z, -1.98412698298579493134e-04, 8.33333333332248946124e-03);
+    const double sb = fma(z, -2.50507602534068634195e-08, 2.75573137070700676789e-06);
+    const double ps = fma(z2, fma(z2, 1.58969099521155010221e-10, sb), sa);
+    const double s = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
+    const double ca = fma(z, -1.38888888888741095749e-03, 4.16666666666666019037e-02);
+    const double cb = fma(z, -2.75573143513906633035e-07, 2.48015872894767294178e-05);
+    const double c3 = fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    const double pc = z * fma(z2, fma(z2, c3, cb), ca);
+#endif
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double c = w + (((1.0 - w) - hz) + z * pc);
@@ -65,6 +79,100 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
 }
 
 CTR_HD bool sincos_needs_slow(double x) { return !(fabs(x) < 1048576.0); }
+
+// Table-based sincos: x = n (pi/32) + r, |r| <= pi/64, with (sin, cos)(k pi/32), k = n mod 64,
+// from a 1 KB table (kept in LDS by the kernels) and short Taylor kernels on r:
+//   sin x = S_k cos r + C_k sin r,   cos x = C_k cos r - S_k sin r.
+// Fewer instructions than sincos_fast (no quadrant selects, degree 9 / 8 instead of 13 / 14),
+// which matters because one wave per SIMD makes the FK loop issue-bound.  Max error <= 2 ulp
+// (tests/test_math.py).  Valid for |x| < 2^20 like sincos_fast.
+constexpr double TRIG_TAB[64][2] = {
+    {0x0.0p+0, 0x1.0000000000000p+0},
+    {0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
+    {0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1},
+    {0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1},
+    {0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1},
+    {0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1},
+    {0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1},
+    {0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1},
+    {0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1},
+    {0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1},
+    {0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1},
+    {0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2},
+    {0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2},
+    {0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
+    {0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3},
+    {0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4},
+    {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4},
+    {0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3},
+    {0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2},
+    {0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2},
+    {0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2},
+    {0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1},
+    {0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1},
+    {0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1},
+    {0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1},
+    {0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1},
+    {0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1},
+    {0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1},
+    {0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1},
+    {0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1},
+    {0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1},
+    {0x0.0p+0, -0x1.0000000000000p+0},
+    {-0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1},
+    {-0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1},
+    {-0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1},
+    {-0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1},
+    {-0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1},
+    {-0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1},
+    {-0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1},
+    {-0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1},
+    {-0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1},
+    {-0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1},
+    {-0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2},
+    {-0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2},
+    {-0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2},
+    {-0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3},
+    {-0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4},
+    {-0x1.0000000000000p+0, 0x0.0p+0},
+    {-0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4},
+    {-0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3},
+    {-0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
+    {-0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2},
+    {-0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2},
+    {-0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1},
+    {-0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1},
+    {-0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1},
+    {-0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1},
+    {-0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1},
+    {-0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1},
+    {-0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1},
+    {-0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1},
+    {-0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1},
+    {-0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
+};
+
+CTR_HD void sincos_tab(double x, const double (*tab)[2], double &sv, double &cv)
+{
+    const double n = rint(x * 10.185916357881302);            // round(x * 32/pi)
+    double r = fma(-n, 0.09817477042468103, x);                // pi/32 = P1 + P2 + P3 (pi/2 split / 16)
+    r = fma(-n, 3.827021247335479e-18, r);
+    r = fma(-n, -9.358655655369811e-35, r);
+    const int k = ((int)n) & 63;
+    const double z = r * r;
+    // sin r = r + r z (-1/6 + z (1/120 + z (-1/5040 + z / 362880)))      |r| <= 0.0491
+    const double sp = fma(z, fma(z, fma(z, 2.7557319223985893e-06, -1.9841269841269841e-04),
+                                 8.3333333333333332e-03), -1.6666666666666666e-01);
+    const double sr = fma(r * z, sp, r);
+    // cos r = 1 + z (-1/2 + z (1/24 + z (-1/720 + z / 40320)))
+    const double cp = fma(z, fma(z, fma(z, 2.4801587301587302e-05, -1.3888888888888889e-03),
+                                 4.1666666666666664e-02), -0.5);
+    const double cr = fma(z, cp, 1.0);
+    const double ts = tab[k][0], tc = tab[k][1];
+    sv = fma(ts, cr, tc * sr);
+    cv = fma(tc, cr, -(ts * sr));
+}
 
 CTR_HD void sincos_cw(double x, double *sp, double *cp)
 {

@@ -13,12 +13,15 @@ def _lib(tmp_path):
     src = tmp_path / "m.cpp"
     src.write_text('#include "ctr_math.hpp"\n'
                    'extern "C" void vsincos(const double* x, double* s, double* c, long n) {\n'
-                   '  for (long i = 0; i < n; ++i) ctr_math::sincos_cw(x[i], s + i, c + i); }\n')
+                   '  for (long i = 0; i < n; ++i) ctr_math::sincos_cw(x[i], s + i, c + i); }\n'
+                   'extern "C" void vsincos_tab(const double* x, double* s, double* c, long n) {\n'
+                   '  for (long i = 0; i < n; ++i) ctr_math::sincos_tab(x[i], ctr_math::TRIG_TAB, s[i], c[i]); }\n')
     so = tmp_path / "m.so"
     subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-shared", "-fPIC",
                            "-I", os.path.join(ROOT, "gym-ctr-reach_amd", "csrc"), str(src), "-o", str(so)])
     lib = ctypes.CDLL(str(so))
     lib.vsincos.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_long]
+    lib.vsincos_tab.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_long]
     return lib
 
 
@@ -26,15 +29,22 @@ def _ulp_err(got, want):
     return np.abs(got - want) / np.spacing(np.maximum(np.abs(want), 1e-300))
 
 
-def test_sincos_cw_accuracy(tmp_path):
+import pytest
+
+
+@pytest.mark.parametrize("fn", ["vsincos", "vsincos_tab"])
+def test_sincos_accuracy(tmp_path, fn):
     lib = _lib(tmp_path)
     rng = np.random.default_rng(0)
     x = np.concatenate([rng.uniform(-np.pi, np.pi, 200000), rng.uniform(-300, 300, 200000),
-                        rng.uniform(-1e5, 1e5, 50000), np.array([0.0, -0.0, 1e-300, np.pi / 2, -np.pi, 1e6, 3e7]),
-                        np.arange(-40, 41) * (np.pi / 2), np.arange(-40, 41) * (np.pi / 2) + 1e-9])
+                        rng.uniform(-1e5, 1e5, 50000), np.array([0.0, -0.0, 1e-300, np.pi / 2, -np.pi]),
+                        np.arange(-40, 41) * (np.pi / 2), np.arange(-40, 41) * (np.pi / 2) + 1e-9,
+                        np.arange(-400, 401) * (np.pi / 32), np.arange(-400, 401) * (np.pi / 32) + 1e-12])
+    if fn == "vsincos":          # sincos_cw has the exact large-argument path; sincos_tab is |x| < 2^20
+        x = np.concatenate([x, [1e6, 3e7]])
     s = np.empty_like(x)
     c = np.empty_like(x)
-    lib.vsincos(x.ctypes.data, s.ctypes.data, c.ctypes.data, len(x))
+    getattr(lib, fn)(x.ctypes.data, s.ctypes.data, c.ctypes.data, len(x))
     # absolute error bound (values near zero crossings) + ulp bound elsewhere
     es = np.abs(s - np.sin(x))
     ec = np.abs(c - np.cos(x))
