@@ -606,14 +606,14 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         double en2 = 0.0;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp1(fma(fmax(fabs(yu[i]), fabs(nu[i])), RTOL, ATOL));
-            const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp1(fma(fmax(fabs(ya[i]), fabs(na[i])), RTOL, ATOL));
-            const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp1(fma(fmax(fabs(yr[i]), fabs(nr[i])), RTOL, ATOL));
+            const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp1(fma(ctr_math::absmax(yu[i], nu[i]), RTOL, ATOL));
+            const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp1(fma(ctr_math::absmax(ya[i], na[i]), RTOL, ATOL));
+            const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp1(fma(ctr_math::absmax(yr[i], nr[i]), RTOL, ATOL));
             en2 = fma(xu, xu, fma(xa, xa, fma(xr, xr, en2)));
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp1(fma(fmax(fabs(yR[i]), fabs(nR[i])), RTOL, ATOL));
+            const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp1(fma(ctr_math::absmax(yR[i], nR[i]), RTOL, ATOL));
             en2 = fma(xR, xR, en2);
         }
         en2 *= h * h;                       // = 18 error_norm^2

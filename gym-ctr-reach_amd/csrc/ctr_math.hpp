@@ -199,6 +199,19 @@ CTR_HD double rcp(double x)
 #endif
 }
 
+// max(|a|, |b|) as one v_max_f64 with abs modifiers (fmax() would first canonicalize each
+// loop-carried operand with an extra v_max: the error scales of the step controller).
+CTR_HD double absmax(double a, double b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmax(fabs(a), fabs(b));
+#endif
+}
+
 // 1/x to about 1 ulp with a single Newton-Raphson step (step-size control only).
 CTR_HD double rcp1(double x)
 {
