@@ -54,14 +54,23 @@ def parse():
 
 
 def dist_init():
+    """One process per GPU (torchrun).  RCCL (backend "nccl") by default.  Rehearsal overrides for
+    a one-GPU box: CTR_BENCH_BACKEND=gloo with CTR_BENCH_SAME_DEVICE=1 puts every rank on cuda:0
+    (RCCL refuses two ranks on one GPU); the timing logic is the same."""
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("CTR_BENCH_SAME_DEVICE") == "1":
+        local = 0
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("CTR_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         return dist, rank, ws, local
     return None, 0, 1, local
 
@@ -167,7 +176,8 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    el = D.max_over_ranks(time.perf_counter() - t0, device=dev)
+    el = D.max_over_ranks(time.perf_counter() - t0,
+                          device=dev if os.environ.get("CTR_BENCH_BACKEND", "nccl") == "nccl" else "cpu")
     total_steps = n * ws * args.steps
 
     # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset
