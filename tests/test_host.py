@@ -128,3 +128,43 @@ def test_config_encoding():
     assert cfg.systems[2].EI[1] == t.E * t.I and cfg.systems[2].GJ[1] == t.G * t.J
     with pytest.raises(ValueError):
         systems.make_config(sysl * 3)
+
+
+def test_new_entry_points_validate_arguments_without_gpu():
+    """ctr_jacobian / ctr_fk_shape / ctr_fk_tables / ctr_domain_params reject bad arguments before
+    touching the device (no GPU needed)."""
+    from ctr_reach_amd import _abi, systems
+    lib = _abi.load()
+    cfg = systems.make_config(systems.tubes_from_params(systems.default_systems_parameters())[:1])
+    p = ctypes.c_void_p(1)
+    assert lib.ctr_jacobian(p, None, 4, cfg, 0.0, None, p, None, None) == -1          # eps = 0
+    assert b"eps" in lib.ctr_last_error()
+    assert lib.ctr_jacobian(None, None, 4, cfg, 1e-4, None, p, None, None) == -1      # no joints
+    assert lib.ctr_jacobian(None, None, 0, cfg, 1e-4, None, None, None, None) == 0     # empty
+    assert lib.ctr_fk_tables(p, None, 4, cfg, p, None, None, None) == -1              # no tables
+    assert lib.ctr_fk_shape(p, None, None, 4, cfg, 270, p, None, None, p, None, None) == -1   # no r/s
+    rk4 = systems.make_config(systems.tubes_from_params(systems.default_systems_parameters())[:1],
+                              integrator=_abi.CTR_INTEGRATOR_RK4, rk4_steps_per_m=100)
+    assert lib.ctr_fk_shape(p, None, None, 4, rk4, 270, p, p, p, p, None, None) == -1
+    assert b"rk45" in lib.ctr_last_error()
+    bad = systems.make_config(systems.tubes_from_params(systems.default_systems_parameters())[:1],
+                              integrator=_abi.CTR_INTEGRATOR_RK4, rk4_steps_per_m=0)
+    assert lib.ctr_fk(p, None, 4, bad, p, None, None, None) == -1                     # RK4 without steps
+    cfg.domain_rand = float("nan")
+    assert lib.ctr_domain_params(cfg, _abi.CtrBatch(), p, None, None) == -1
+    cfg.domain_rand = 0.05
+    b = _abi.CtrBatch()
+    b.n = 4
+    assert lib.ctr_domain_params(cfg, b, p, None, None) == -1                         # no system/epoch
+
+
+def test_solver_kwargs_validation():
+    from ctr_reach_amd.systems import solver_codes
+    assert solver_codes("rk45_scipy", 0, "compliant") == (0, 0, 0)
+    assert solver_codes("rk4", 100, "rigid") == (1, 100, 1)
+    with pytest.raises(ValueError):
+        solver_codes("rk4", 0, "compliant")
+    with pytest.raises(ValueError):
+        solver_codes("euler", 10, "compliant")
+    with pytest.raises(ValueError):
+        solver_codes("rk45_scipy", 0, "stiff")
