@@ -190,20 +190,23 @@ __device__ __forceinline__ void trig_table_fill()
 __device__ __forceinline__ void trig_table_fill() {}
 #endif
 
+// CAREFUL: a wave-uniform ballot sends huge / non-finite angle differences (|d| >= 2^20) to the
+// exact out-of-line path.  The branch splits the stage code into basic blocks the scheduler
+// cannot interleave (measured +6 % on k_step), so the FK checks its joint angles once
+// (fk_needs_careful_trig) and runs the CAREFUL variant only when some lane of the wave needs it.
+template <bool CAREFUL = true>
 __device__ __forceinline__ Trig trig_of(const double al[3])
 {
     Trig t;
     const double d10 = al[1] - al[0], d20 = al[2] - al[0];
-    // both reductions branch-free and interleavable; the exact slow path only when some lane
-    // of the wave has a huge / non-finite angle (wave-uniform branch)
 #ifndef CTR_TRIG_POLY
-    ctr_math::sincos_tab(d10, s_trig_tab, t.s10, t.c10);
-    ctr_math::sincos_tab(d20, s_trig_tab, t.s20, t.c20);
+    ctr_math::sincos_tab2(d10, d20, s_trig_tab, t.s10, t.c10, t.s20, t.c20);
 #else
     ctr_math::sincos_fast(d10, t.s10, t.c10);
     ctr_math::sincos_fast(d20, t.s20, t.c20);
 #endif
-    if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10) || ctr_math::sincos_needs_slow(d20)) != 0, 0)) {
+    if (CAREFUL &&
+        __builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10) || ctr_math::sincos_needs_slow(d20)) != 0, 0)) {
         if (ctr_math::sincos_needs_slow(d10)) {
             const ctr_math::SinCos r = ctr_math::sincos_slow(d10);
             t.s10 = r.s;
@@ -219,6 +222,16 @@ __device__ __forceinline__ Trig trig_of(const double al[3])
     t.c21 = t.c20 * t.c10 + t.s20 * t.s10;
     t.s21 = t.s20 * t.c10 - t.c20 * t.s10;
     return t;
+}
+
+// Wave-uniform: does some lane start the FK with an angle of magnitude >= 2^18 (or non-finite)?
+// Otherwise every angle difference met during the FK stays below 2^20: the twist integrated over
+// a backbone (<= ~0.5 m) moves an angle by orders of magnitude less than 2^18 rad.
+__device__ __forceinline__ bool fk_needs_careful_trig(const double q[6])
+{
+    const double lim = 262144.0;
+    const bool ok = fabs(q[3]) < lim && fabs(q[4]) < lim && fabs(q[5]) < lim;
+    return __ballot(!ok) != 0;
 }
 
 template <bool HAS_UY>
@@ -359,7 +372,7 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
 // Forward kinematics of one lane, scipy-RK45 integrator: joints (f64; the env's float32 joints
 // promoted exactly as model.py:51 does) -> tip (f64).  RIGID: torsionally rigid variant (GJ -> inf:
 // u_z stays 0, the tube angles stay at their joint values, so the trig is computed once).
-template <bool HAS_UY, bool RIGID, bool SHAPE = false>
+template <bool HAS_UY, bool RIGID, bool SHAPE = false, bool CAREFUL = true>
 __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st, ShapeOut *so = nullptr)
 {
     using namespace rk;
@@ -380,7 +393,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         yR[3] = s0; yR[4] = c0;  yR[5] = 0.0;
         yR[6] = 0.0; yR[7] = 0.0; yR[8] = 1.0;
     }
-    Trig ty = trig_of(ya);          // trig of the current state's alphas (reused at segment starts)
+    Trig ty = trig_of<CAREFUL>(ya);          // trig of the current state's alphas (reused at segment starts)
     Stage f;                        // FSAL derivative at y (alpha' and r' implied by y)
     SegPar p;
     double t = 0.0, tb = 0.0, ha = 0.0, min_step = 0.0, prev_end = 0.0;
@@ -478,7 +491,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             Stage f1;
             double f1r[3];
             {
-                const Trig t1 = RIGID ? ty : trig_of(a1);
+                const Trig t1 = RIGID ? ty : trig_of<CAREFUL>(a1);
                 rhs_core<HAS_UY>(p, t1, u1, R1, f1.uz, f1.R);
                 stage_at(p, t1, u1, R1, f1, f1r);
             }
@@ -551,7 +564,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
                 ai[i] = EXPR_A;                                                                \
             }                                                                                  \
             _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = EXPR_R;                      \
-            const Trig tt = RIGID ? ty : trig_of(ai);                                          \
+            const Trig tt = RIGID ? ty : trig_of<CAREFUL>(ai);                                \
             rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
             stage_at(p, tt, ui, Ri, KOUT, rc);                                                 \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
@@ -598,7 +611,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         }
         Stage K6;
         double k6r[3];
-        const Trig tn = RIGID ? ty : trig_of(na);
+        const Trig tn = RIGID ? ty : trig_of<CAREFUL>(na);
         rhs_core<HAS_UY>(p, tn, nu, nR, K6.uz, K6.R);
         stage_at(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
@@ -685,7 +698,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 // n = max(1, ceil((tb - t0) * steps_per_m)) equal steps.  Lanes stay in lock-step: one loop
 // iteration = one RK4 step of whichever segment the lane is in.
 // ------------------------------------------------------------------------------------------
-template <bool HAS_UY, bool RIGID>
+template <bool HAS_UY, bool RIGID, bool CAREFUL = true>
 __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], FkStats &st, double steps_per_m)
 {
     const double beta[3] = {q[0], q[1], q[2]};
@@ -703,7 +716,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
         yR[3] = s0; yR[4] = c0;  yR[5] = 0.0;
         yR[6] = 0.0; yR[7] = 0.0; yR[8] = 1.0;
     }
-    const Trig tconst = trig_of(ya);     // RIGID: the tube angles never change
+    const Trig tconst = trig_of<CAREFUL>(ya);     // RIGID: the tube angles never change
     SegPar p;
     double h = 0.0, prev_end = 0.0;
     int left = 0;                        // RK4 steps left in the current segment
@@ -727,7 +740,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
         double r1[3], r2[3], r3[3], r4[3];
         double ui[3], ai[3], Ri[9];
         {
-            const Trig tt = RIGID ? tconst : trig_of(ya);
+            const Trig tt = RIGID ? tconst : trig_of<CAREFUL>(ya);
             rhs_core<HAS_UY>(p, tt, yu, yR, k1.uz, k1.R);
             stage_at(p, tt, yu, yR, k1, r1);
         }
@@ -739,7 +752,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
                 ai[i] = fma(KIN.al[i], C, ya[i]);                                              \
             }                                                                                  \
             _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = fma(KIN.R[i], C, yR[i]);     \
-            const Trig tt = RIGID ? tconst : trig_of(ai);                                      \
+            const Trig tt = RIGID ? tconst : trig_of<CAREFUL>(ai);                                \
             rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
             stage_at(p, tt, ui, Ri, KOUT, ROUT);                                               \
         }

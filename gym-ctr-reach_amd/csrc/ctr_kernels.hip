@@ -107,8 +107,15 @@ template <int MODE>
 __device__ __forceinline__ void fk_dispatch_d(const KCfg &kc, const SysK &sy, const double qd[6], double tip[3],
                                               FkStats &st)
 {
-    if (MODE & 2) fk_lane_rk4<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st, (double)kc.c.rk4_steps_per_m);
-    else fk_lane<(MODE & 1) != 0, (MODE & 4) != 0>(sy, qd, tip, st);
+    constexpr bool UY = (MODE & 1) != 0, RG = (MODE & 4) != 0;
+    const bool careful = fk_needs_careful_trig(qd);
+    if (MODE & 2) {
+        if (careful) fk_lane_rk4<UY, RG, true>(sy, qd, tip, st, (double)kc.c.rk4_steps_per_m);
+        else fk_lane_rk4<UY, RG, false>(sy, qd, tip, st, (double)kc.c.rk4_steps_per_m);
+    } else {
+        if (careful) fk_lane<UY, RG, false, true>(sy, qd, tip, st);
+        else fk_lane<UY, RG, false, false>(sy, qd, tip, st);
+    }
 }
 
 // Model.forward_kinematics widens the float32 joints of Obs to float64 (model.py:48-62).
@@ -220,7 +227,8 @@ __global__ __launch_bounds__(BLOCK) void k_fk_shape(KCfg kc, const float *__rest
         FkStats st = {0, 0, 0, 0, 0};
         ShapeOut so = {r + (int64_t)3 * cap * e, s_out + (int64_t)cap * e, cap, 0};
         double out[3];
-        fk_lane<(MODE & 1) != 0, (MODE & 4) != 0, true>(*sy, q, out, st, &so);
+        if (fk_needs_careful_trig(q)) fk_lane<(MODE & 1) != 0, (MODE & 4) != 0, true, true>(*sy, q, out, st, &so);
+        else fk_lane<(MODE & 1) != 0, (MODE & 4) != 0, true, false>(*sy, q, out, st, &so);
         #pragma unroll
         for (int i = 0; i < 3; ++i) tip[3 * e + i] = out[i];
         npts[e] = so.count;

@@ -153,6 +153,37 @@ constexpr double TRIG_TAB[64][2] = {
     {-0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
 };
 
+// Two angles at once: both reductions and both table loads are issued before either pair of
+// Taylor kernels, so the LDS latency of the table reads hides behind the polynomial work.
+CTR_HD void sincos_tab2(double x0, double x1, const double (*tab)[2], double &s0, double &c0, double &s1,
+                        double &c1)
+{
+    const double n0 = rint(x0 * 10.185916357881302), n1 = rint(x1 * 10.185916357881302);
+    const int k0 = ((int)n0) & 63, k1 = ((int)n1) & 63;
+    const double ts0 = tab[k0][0], tc0 = tab[k0][1];
+    const double ts1 = tab[k1][0], tc1 = tab[k1][1];
+    double r0 = fma(-n0, 0.09817477042468103, x0), r1 = fma(-n1, 0.09817477042468103, x1);
+    r0 = fma(-n0, 3.827021247335479e-18, r0);
+    r1 = fma(-n1, 3.827021247335479e-18, r1);
+    r0 = fma(-n0, -9.358655655369811e-35, r0);
+    r1 = fma(-n1, -9.358655655369811e-35, r1);
+    const double z0 = r0 * r0, z1 = r1 * r1;
+    const double sp0 = fma(z0, fma(z0, fma(z0, 2.7557319223985893e-06, -1.9841269841269841e-04),
+                                   8.3333333333333332e-03), -1.6666666666666666e-01);
+    const double sp1 = fma(z1, fma(z1, fma(z1, 2.7557319223985893e-06, -1.9841269841269841e-04),
+                                   8.3333333333333332e-03), -1.6666666666666666e-01);
+    const double cp0 = fma(z0, fma(z0, fma(z0, 2.4801587301587302e-05, -1.3888888888888889e-03),
+                                   4.1666666666666664e-02), -0.5);
+    const double cp1 = fma(z1, fma(z1, fma(z1, 2.4801587301587302e-05, -1.3888888888888889e-03),
+                                   4.1666666666666664e-02), -0.5);
+    const double sr0 = fma(r0 * z0, sp0, r0), sr1 = fma(r1 * z1, sp1, r1);
+    const double cr0 = fma(z0, cp0, 1.0), cr1 = fma(z1, cp1, 1.0);
+    s0 = fma(ts0, cr0, tc0 * sr0);
+    c0 = fma(tc0, cr0, -(ts0 * sr0));
+    s1 = fma(ts1, cr1, tc1 * sr1);
+    c1 = fma(tc1, cr1, -(ts1 * sr1));
+}
+
 CTR_HD void sincos_tab(double x, const double (*tab)[2], double &sv, double &cv)
 {
     const double n = rint(x * 10.185916357881302);            // round(x * 32/pi)

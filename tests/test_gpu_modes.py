@@ -97,3 +97,27 @@ def test_tube_gap_nan_status(cuda):
     tip, st = env.forward_kinematics(np.array([GAP_JOINTS], np.float32), return_stats=True)
     assert np.isnan(tip.cpu().numpy()).all()
     assert st["status"].cpu().numpy()[0] & 4
+
+
+def test_fk_huge_angles_vs_oracle(cuda, oracle_mod):
+    """Joint angles of magnitude >= 2^18 (e.g. alpha accumulated over many episodes without
+    resampling) take the wave-uniform careful path: exact large-argument sin/cos for any angle
+    difference >= 2^20.  Mixed with ordinary waves; tips vs the oracle (libm sin/cos)."""
+    from ctr_reach_amd import CtrReachVecEnv
+    n = 4096
+    q, sysid = _joints(oracle_mod, n, 31)
+    rng = np.random.default_rng(2)
+    big = np.zeros(n, bool)
+    big[:64] = True                           # the first wave: every lane huge
+    big[64 * 5 + 3] = True                    # one lane of another wave
+    big[64 * 9:64 * 9 + 32] = True            # half a wave
+    q[big, 3:] = (rng.choice([-1, 1], (big.sum(), 3)) * rng.uniform(3e5, 3e6, (big.sum(), 3))).astype(np.float32)
+    env = CtrReachVecEnv(1, device=cuda, select_systems=[0, 1, 2, 3])
+    tip, st = env.forward_kinematics(q, sysid, return_stats=True)
+    ref = oracle_mod.fk(q, sysid)
+    err = np.linalg.norm(tip.cpu().numpy() - ref["tip"], axis=1)
+    # at |alpha| ~ 1e6 one ulp of an angle is ~1e-10 rad: FMA vs separately rounded stage angles
+    # move the tip by up to ~1e-8 m; ordinary lanes keep the usual agreement
+    assert err[big].max() < 1e-6, err[big].max()
+    assert err[~big].max() < 1e-10, err[~big].max()
+    assert np.isfinite(tip.cpu().numpy()).all()
