@@ -110,6 +110,31 @@ def fk_work(env, joints):
     return flops, sincos, nfev.mean().item()
 
 
+def parity_probe(env, cfgd):
+    """tip-position L2 of the GPU FK against the CPU restatement of the reference
+    (oracle/, pinned to the reference's fixtures) on every env's current joints, and agreement of
+    the reached flag outside a +-1e-6 m band around tol.  Part of the CPU leg (rank 0, N = 1)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    q = env.joints.detach().cpu().numpy()
+    sysid = env.system.detach().cpu().numpy()
+    dg = env.desired_goal.detach().cpu().numpy()
+    tip = env.forward_kinematics(env.joints, env.system).cpu().numpy()
+    ref = oracle.fk(q, sysid, integrator=cfgd["integrator"], steps_per_m=cfgd["rk4_steps_per_m"],
+                    model=cfgd["model"])["tip"]
+    l2 = np.linalg.norm(tip - ref, axis=1)
+    tol = env.goal_tolerance.get_tol()
+    d_gpu = np.linalg.norm(tip - dg, axis=1)
+    d_cpu = np.linalg.norm(ref - dg, axis=1)
+    outside = np.abs(d_cpu - tol) > 1e-6
+    agree = ((d_gpu < tol) == (d_cpu < tol))[outside].mean() if outside.any() else 1.0
+    return {"envs": int(q.shape[0]), "tip_l2_max_m": float(l2.max()), "tip_l2_p999_m": float(np.quantile(l2, 0.999)),
+            "reached_flag_agreement": float(agree), "band_m": 1e-6,
+            "checker": "oracle/ctr_oracle.c (CPU restatement, pinned to the reference's fixtures)"}
+
+
 def cpu_baseline(args, cfgd):
     """Oracle (C port, OpenMP) on this host: env-steps/s on a bounded sample of the workload."""
     import numpy as np
@@ -234,6 +259,7 @@ def main():
         if t.get("envs") == n and t.get("config", 3) == args.config:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
     if not args.no_cpu_baseline and ws == 1:
+        out["parity"] = parity_probe(env, cfgd)
         out["cpu_baseline"] = cpu_baseline(args, cfgd)
     print(json.dumps(out))
     if dist:

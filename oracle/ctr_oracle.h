@@ -44,6 +44,8 @@ void oracle_jacobian(const double *joints, const int32_t *sys_idx, int64_t n, co
                      int integrator, int steps_per_m, int rigid, double eps, double *tip, double *jac);
 void oracle_fk_shape(const float *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
                      int cap, double *tip, double *r, double *s, int32_t *npts, int32_t *status);
+void oracle_fk_segattempts(const float *joints, const int32_t *sys_idx, int64_t n, const oracle_system_t *systems,
+                           int32_t *att);
 int oracle_version(void);
 
 #ifdef __cplusplus

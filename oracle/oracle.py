@@ -48,6 +48,7 @@ def lib():
         L.oracle_segments.argtypes = [P, P, i64, P, P, P]
         L.oracle_jacobian.argtypes = [P, P, i64, P, ci, ci, ci, ctypes.c_double, P, P]
         L.oracle_fk_shape.argtypes = [P, P, i64, P, ci, P, P, P, P, P]
+        L.oracle_fk_segattempts.argtypes = [P, P, i64, P, P]
         L.oracle_domain_systems.argtypes = [i64, P, P, P, P, ctypes.c_double, u64, P, i64, P]
         _lib = L
     return _lib
@@ -138,6 +139,17 @@ def fk_shape(joints, system=None, systems=None, cap=270):
     lib().oracle_fk_shape(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), int(cap), _p(tip), _p(r), _p(sv),
                           _p(npts), _p(status))
     return dict(tip=tip, r=r, s=sv, npts=npts, status=status)
+
+
+def fk_segattempts(joints, system=None, systems=None):
+    """Diagnostic: RK45 attempts per integrated segment, [n, 9]."""
+    q = np.ascontiguousarray(joints, dtype=np.float32).reshape(-1, 6)
+    n = q.shape[0]
+    s = None if system is None else np.ascontiguousarray(np.broadcast_to(system, (n,)), dtype=np.int32)
+    systems = systems if systems is not None else make_systems()
+    att = np.zeros((n, 9), np.int32)
+    lib().oracle_fk_segattempts(_p(q), _p(s), n, ctypes.cast(systems, ctypes.c_void_p), _p(att))
+    return att
 
 
 def tube_tip_indices(s, L, beta):
