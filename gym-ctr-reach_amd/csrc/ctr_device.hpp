@@ -481,7 +481,9 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             }
             // d0 = ||y/sc||_rms, d1 = ||f/sc||_rms kept squared (no sqrt on the hot path)
             const double d0sq = s0 * (1.0 / 18), d1sq = s1 * (1.0 / 18);
-            double h0 = (d0sq < 1e-10 || d1sq < 1e-10) ? 1e-6 : 0.01 * ctr_math::sqrt_rsq(s0 * ctr_math::rcp1(s1));
+            // branch-free selects (both sides are cheap; a branch would split the scheduling region)
+            const double h0n = 0.01 * ctr_math::sqrt_rsq(s0 * ctr_math::rcp1(s1));
+            double h0 = (d0sq < 1e-10 || d1sq < 1e-10) ? 1e-6 : h0n;
             h0 = fmin(h0, interval);
             double u1[3], a1[3], R1[9];
             #pragma unroll
@@ -511,8 +513,9 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             const double ih0 = ctr_math::rcp1(h0);
             const double d2sq = s2 * (1.0 / 18) * ih0 * ih0;            // d2^2
             double h1;
-            if (d1sq <= 1e-30 && d2sq <= 1e-30) h1 = fmax(1e-6, h0 * 1e-3);
-            else h1 = 0.3981071705534972 * ctr_math::inv_root10(fmax(d1sq, d2sq));   // (0.01/max(d1,d2))^(1/5)
+            const double h1a = fmax(1e-6, h0 * 1e-3);
+            const double h1b = 0.3981071705534972 * ctr_math::inv_root10(fmax(d1sq, d2sq));   // (0.01/max(d1,d2))^(1/5)
+            h1 = (d1sq <= 1e-30 && d2sq <= 1e-30) ? h1a : h1b;
             ha = fmin(fmin(100.0 * h0, h1), interval);
             t = t0;
             need_init = false;
@@ -521,10 +524,12 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 
         CTR_STAMP(ts1);
         // ---- one attempt of RungeKutta._step_impl (rk.py:111-175) ----
-        if (new_step) {
-            min_step = 10.0 * fabs(nextafter(t, INFINITY) - t);
-            if (ha < min_step) ha = min_step;
-            rejected = false;
+        {
+            // new step: min_step = 10 |nextafter(t, inf) - t| and h_abs >= min_step (rk.py:114-119)
+            const double ms = 10.0 * fabs(nextafter(t, INFINITY) - t);
+            min_step = new_step ? ms : min_step;
+            ha = (new_step && ha < ms) ? ms : ha;
+            rejected = new_step ? false : rejected;
             new_step = false;
         }
         if (ha < min_step) {                         // TOO_SMALL_STEP -> solver failed
