@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--profile-only", action="store_true", help="no timing extras (for rocprofv3)")
+    ap.add_argument("--refill-interval", type=int, default=None, help="reset-pool refill interval (steps)")
     return ap.parse_args()
 
 
@@ -176,8 +177,10 @@ def main():
     torch.cuda.set_device(dev)
     cfgd = CONFIGS[args.config]
     n = args.envs or cfgd["envs"]
+    extra = {} if args.refill_interval is None else {"refill_interval": args.refill_interval}
     env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
-                         integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"])
+                         integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"],
+                         **extra)
     env.reset()
     acts = make_actions(env, 8, args.seed + rank)
     stream = torch.cuda.current_stream()

@@ -84,7 +84,7 @@ class CtrReachVecEnv(object):
     reference's torsionally-compliant ODE, model.py:72-117) or "rigid" (GJ -> infinity)."""
 
     def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
-                 pool_depth=None, refill_interval=32, integrator="rk45_scipy", rk4_steps_per_m=100,
+                 pool_depth=None, refill_interval=64, integrator="rk45_scipy", rk4_steps_per_m=100,
                  model="compliant", **kwargs):
         torch = _torch()
         kw = default_kwargs()
