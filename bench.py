@@ -39,7 +39,7 @@ BYTES_STEP = 170        # algorithmic bytes per env-step
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=128, help="timed steps (a multiple of the 64-step pool refill by default)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 5),
                     help="BASELINE.json config (1-based): 3 = headline (65 536 envs, compliant, scipy RK45); "
@@ -246,7 +246,8 @@ def main():
                                                      "auto-reset",
                    "integrator": cfgd["integrator"], "model": cfgd["model"],
                    "rk4_steps_per_m": cfgd["rk4_steps_per_m"] if cfgd["integrator"] == "rk4" else None,
-                   "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws},
+                   "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
+                   "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval}},
         "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": PEAK_FP64_VALU, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_VALU, "traffic": None,
                      "kernel": "k_step", "kernel_ms": k_ms,
