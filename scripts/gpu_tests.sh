@@ -9,7 +9,7 @@ run() {   # run <name> <seconds> <cmd...>
     echo "$name rc=$rc"; tail -${TAILN:-4} "gpurun_out/$name.log"
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "abnormal exit, stopping"; exit $rc; fi
 }
-TAILN=30 run pytest_gpu 600 python -m pytest tests -m gpu -q
+TAILN=30 run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 400 python bench.py --steps 20 --warmup 5 --cpu-seconds 5
 run bench_c2 300 python bench.py --config 2 --steps 20 --warmup 5 --cpu-seconds 5
