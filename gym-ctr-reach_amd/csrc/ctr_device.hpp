@@ -142,6 +142,7 @@ __device__ __forceinline__ void sysk_derive(SysK &s, int j)
 // product ei[j] * ux_0[j] (model.py:85-90); kz = EI/GJ (model.py:97).
 struct SegPar {
     double wx[3], wy[3], ux0[3], uy0[3], kz[3], inv;
+    double g[3];       // no y pre-curvature: du_z,j/ds = g_j * (sum_k wx_k sin(alpha_k - alpha_j))
     uint32_t present;  // bit j: tube j present (EI_j != 0)
 };
 
@@ -160,6 +161,8 @@ __device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool r
         p.kz[j] = (pres && !rigid) ? sy.kz[j] : 0.0;   // torsionally rigid: GJ -> infinity
     }
     p.inv = sy.inv[bits6 & 7u];
+    #pragma unroll
+    for (int j = 0; j < 3; ++j) p.g[j] = (p.kz[j] * p.ux0[j]) * p.inv;
     p.present = (uint32_t)(bits6 & 7u);
     return p;
 }
@@ -178,13 +181,13 @@ struct Trig {
 };
 
 #ifndef CTR_TRIG_POLY
-// (sin, cos)(k pi/32) table for sincos_tab, one copy per workgroup in LDS; every kernel that
+// (sin, cos)(k pi/64) table for sincos_tab, one copy per workgroup in LDS; every kernel that
 // integrates calls trig_table_fill() before its first barrier.
-__shared__ double s_trig_tab[64][2];
+__shared__ double s_trig_tab[128][2];
 
 __device__ __forceinline__ void trig_table_fill()
 {
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
 }
 #else
 __device__ __forceinline__ void trig_table_fill() {}
@@ -238,6 +241,30 @@ template <bool HAS_UY>
 __device__ __forceinline__ void rhs_core(const SegPar &p, const Trig &t, const double uz[3], const double R[9],
                                          double duz[3], double dR[9])
 {
+    if constexpr (!HAS_UY) {
+        // No tube has y pre-curvature (U_y = 0, the registered systems): model.py:86-102 reduce to
+        //   uy_i = inv * sum_{k != i} wx_k sin(alpha_k - alpha_i)      (the sign folded per row)
+        //   du_z,i/ds = -kz_i ux0_i uy_i = g_i * sum_{k != i} wx_k sin(alpha_i - alpha_k)
+        // and only ux_0 of the x curvatures is used (the frame).  Same quantities as the general
+        // form below with the known zero / unit terms dropped (a few ulp apart).
+        const double sy1 = fma(p.wx[2], t.s20, p.wx[1] * t.s10);         // = -sum_k wx_k s[0][k]
+        const double sy2 = fma(p.wx[2], t.s21, -(p.wx[0] * t.s10));       // = -sum_k wx_k s[1][k]
+        const double sy3 = fma(p.wx[1], t.s21, p.wx[0] * t.s20);          // = +sum_k wx_k s[2][k]
+        duz[0] = -(p.g[0] * sy1);
+        duz[1] = -(p.g[1] * sy2);
+        duz[2] = p.g[2] * sy3;
+        const double a = p.inv * fma(p.wx[2], t.c20, fma(p.wx[1], t.c10, p.wx[0]));   // ux_0
+        const double b = p.inv * sy1;                                                  // uy_0
+        const double u0 = uz[0];
+        #pragma unroll
+        for (int r = 0; r < 3; ++r) {                             // dR = R [u]x  (model.py:103-110)
+            const double r0 = R[3 * r], r1 = R[3 * r + 1], r2 = R[3 * r + 2];
+            dR[3 * r + 0] = r1 * u0 - r2 * b;
+            dR[3 * r + 1] = r2 * a - r0 * u0;
+            dR[3 * r + 2] = r0 * b - r1 * a;
+        }
+        return;
+    }
     const double c[3][3] = {{1.0, t.c10, t.c20}, {t.c10, 1.0, t.c21}, {t.c20, t.c21, 1.0}};
     const double s[3][3] = {{0.0, -t.s10, -t.s20}, {t.s10, 0.0, -t.s21}, {t.s20, t.s21, 0.0}};
     double ux[3], uy[3];
@@ -460,12 +487,12 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             double isc_u[3], isc_a[3], isc_r[3], isc_R[9];
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                isc_u[i] = ctr_math::rcp1(ATOL + fabs(yu[i]) * RTOL);
-                isc_a[i] = ctr_math::rcp1(ATOL + fabs(ya[i]) * RTOL);
-                isc_r[i] = ctr_math::rcp1(ATOL + fabs(yr[i]) * RTOL);
+                isc_u[i] = ctr_math::rcp_est(ATOL + fabs(yu[i]) * RTOL);
+                isc_a[i] = ctr_math::rcp_est(ATOL + fabs(ya[i]) * RTOL);
+                isc_r[i] = ctr_math::rcp_est(ATOL + fabs(yr[i]) * RTOL);
             }
             #pragma unroll
-            for (int i = 0; i < 9; ++i) isc_R[i] = ctr_math::rcp1(ATOL + fabs(yR[i]) * RTOL);
+            for (int i = 0; i < 9; ++i) isc_R[i] = ctr_math::rcp_est(ATOL + fabs(yR[i]) * RTOL);
             double s0 = 0.0, s1 = 0.0;
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -624,14 +651,14 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         double en2 = 0.0;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp1(fma(ctr_math::absmax(yu[i], nu[i]), RTOL, ATOL));
-            const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp1(fma(ctr_math::absmax(ya[i], na[i]), RTOL, ATOL));
-            const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp1(fma(ctr_math::absmax(yr[i], nr[i]), RTOL, ATOL));
+            const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yu[i], nu[i]), RTOL, ATOL));
+            const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(ya[i], na[i]), RTOL, ATOL));
+            const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yr[i], nr[i]), RTOL, ATOL));
             en2 = fma(xu, xu, fma(xa, xa, fma(xr, xr, en2)));
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp1(fma(ctr_math::absmax(yR[i], nR[i]), RTOL, ATOL));
+            const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yR[i], nR[i]), RTOL, ATOL));
             en2 = fma(xR, xR, en2);
         }
         en2 *= h * h;                       // = 18 error_norm^2

@@ -80,77 +80,142 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
 
 CTR_HD bool sincos_needs_slow(double x) { return !(fabs(x) < 1048576.0); }
 
-// Table-based sincos: x = n (pi/32) + r, |r| <= pi/64, with (sin, cos)(k pi/32), k = n mod 64,
-// from a 1 KB table (kept in LDS by the kernels) and short Taylor kernels on r:
+// Table-based sincos: x = n (pi/64) + r, |r| <= pi/128, with (sin, cos)(k pi/64), k = n mod 128,
+// from a 2 KB table (kept in LDS by the kernels) and short Taylor kernels on r:
 //   sin x = S_k cos r + C_k sin r,   cos x = C_k cos r - S_k sin r.
-// Fewer instructions than sincos_fast (no quadrant selects, degree 9 / 8 instead of 13 / 14),
-// which matters because one wave per SIMD makes the FK loop issue-bound.  Max error <= 2 ulp
-// (tests/test_math.py).  Valid for |x| < 2^20 like sincos_fast.
-constexpr double TRIG_TAB[64][2] = {
+// Degree 7 / 6 kernels (truncation < 4e-18 on |r| <= 0.0246) and a two-term Cody-Waite reduction
+// (the third pi/64 term is below 1e-28 for |x| < 2^20): 16 fp64 operations per angle, no
+// quadrant selects.  One wave per SIMD makes the FK loop issue-bound, so every operation counts.
+// Max error <= 2 ulp (tests/test_math.py).  Valid for |x| < 2^20 like sincos_fast.
+constexpr double TRIG_TAB[128][2] = {
     {0x0.0p+0, 0x1.0000000000000p+0},
+    {0x1.91f65f10dd814p-5, 0x1.ff621e3796d7ep-1},
     {0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
+    {0x1.2c8106e8e613ap-3, 0x1.fa7557f08a517p-1},
     {0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1},
+    {0x1.f19f97b215f1bp-3, 0x1.f0a7efb9230d7p-1},
     {0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1},
+    {0x1.58f9a75ab1fddp-2, 0x1.e212104f686e5p-1},
     {0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1},
+    {0x1.b5d1009e15cc0p-2, 0x1.ced7af43cc773p-1},
     {0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1},
+    {0x1.073879922ffeep-1, 0x1.b728345196e3ep-1},
     {0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1},
+    {0x1.30ff7fce17035p-1, 0x1.9b3e047f38741p-1},
     {0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1},
+    {0x1.57d69348ceca0p-1, 0x1.7b5df226aafafp-1},
     {0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1},
+    {0x1.7b5df226aafafp-1, 0x1.57d69348ceca0p-1},
     {0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1},
+    {0x1.9b3e047f38741p-1, 0x1.30ff7fce17035p-1},
     {0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1},
+    {0x1.b728345196e3ep-1, 0x1.073879922ffeep-1},
     {0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2},
+    {0x1.ced7af43cc773p-1, 0x1.b5d1009e15cc0p-2},
     {0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2},
+    {0x1.e212104f686e5p-1, 0x1.58f9a75ab1fddp-2},
     {0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
+    {0x1.f0a7efb9230d7p-1, 0x1.f19f97b215f1bp-3},
     {0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3},
+    {0x1.fa7557f08a517p-1, 0x1.2c8106e8e613ap-3},
     {0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4},
-    {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.ff621e3796d7ep-1, 0x1.91f65f10dd814p-5},
+    {0x1.0000000000000p+0, 0x1.77d4c76273645p-204},
+    {0x1.ff621e3796d7ep-1, -0x1.91f65f10dd814p-5},
     {0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4},
+    {0x1.fa7557f08a517p-1, -0x1.2c8106e8e613ap-3},
     {0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3},
+    {0x1.f0a7efb9230d7p-1, -0x1.f19f97b215f1bp-3},
     {0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2},
+    {0x1.e212104f686e5p-1, -0x1.58f9a75ab1fddp-2},
     {0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2},
+    {0x1.ced7af43cc773p-1, -0x1.b5d1009e15cc0p-2},
     {0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2},
+    {0x1.b728345196e3ep-1, -0x1.073879922ffeep-1},
     {0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1},
+    {0x1.9b3e047f38741p-1, -0x1.30ff7fce17035p-1},
     {0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1},
+    {0x1.7b5df226aafafp-1, -0x1.57d69348ceca0p-1},
     {0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1},
+    {0x1.57d69348ceca0p-1, -0x1.7b5df226aafafp-1},
     {0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1},
+    {0x1.30ff7fce17035p-1, -0x1.9b3e047f38741p-1},
     {0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1},
+    {0x1.073879922ffeep-1, -0x1.b728345196e3ep-1},
     {0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1},
+    {0x1.b5d1009e15cc0p-2, -0x1.ced7af43cc773p-1},
     {0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1},
+    {0x1.58f9a75ab1fddp-2, -0x1.e212104f686e5p-1},
     {0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1},
+    {0x1.f19f97b215f1bp-3, -0x1.f0a7efb9230d7p-1},
     {0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1},
+    {0x1.2c8106e8e613ap-3, -0x1.fa7557f08a517p-1},
     {0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1},
-    {0x0.0p+0, -0x1.0000000000000p+0},
+    {0x1.91f65f10dd814p-5, -0x1.ff621e3796d7ep-1},
+    {0x1.77d4c76273645p-203, -0x1.0000000000000p+0},
+    {-0x1.91f65f10dd814p-5, -0x1.ff621e3796d7ep-1},
     {-0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1},
+    {-0x1.2c8106e8e613ap-3, -0x1.fa7557f08a517p-1},
     {-0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1},
+    {-0x1.f19f97b215f1bp-3, -0x1.f0a7efb9230d7p-1},
     {-0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1},
+    {-0x1.58f9a75ab1fddp-2, -0x1.e212104f686e5p-1},
     {-0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1},
+    {-0x1.b5d1009e15cc0p-2, -0x1.ced7af43cc773p-1},
     {-0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1},
+    {-0x1.073879922ffeep-1, -0x1.b728345196e3ep-1},
     {-0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1},
+    {-0x1.30ff7fce17035p-1, -0x1.9b3e047f38741p-1},
     {-0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1},
+    {-0x1.57d69348ceca0p-1, -0x1.7b5df226aafafp-1},
     {-0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1},
+    {-0x1.7b5df226aafafp-1, -0x1.57d69348ceca0p-1},
     {-0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1},
+    {-0x1.9b3e047f38741p-1, -0x1.30ff7fce17035p-1},
     {-0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1},
+    {-0x1.b728345196e3ep-1, -0x1.073879922ffeep-1},
     {-0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2},
+    {-0x1.ced7af43cc773p-1, -0x1.b5d1009e15cc0p-2},
     {-0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2},
+    {-0x1.e212104f686e5p-1, -0x1.58f9a75ab1fddp-2},
     {-0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2},
+    {-0x1.f0a7efb9230d7p-1, -0x1.f19f97b215f1bp-3},
     {-0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3},
+    {-0x1.fa7557f08a517p-1, -0x1.2c8106e8e613ap-3},
     {-0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4},
-    {-0x1.0000000000000p+0, 0x0.0p+0},
+    {-0x1.ff621e3796d7ep-1, -0x1.91f65f10dd814p-5},
+    {-0x1.0000000000000p+0, 0x1.dcc40d4ec52eap-199},
+    {-0x1.ff621e3796d7ep-1, 0x1.91f65f10dd814p-5},
     {-0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4},
+    {-0x1.fa7557f08a517p-1, 0x1.2c8106e8e613ap-3},
     {-0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3},
+    {-0x1.f0a7efb9230d7p-1, 0x1.f19f97b215f1bp-3},
     {-0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
+    {-0x1.e212104f686e5p-1, 0x1.58f9a75ab1fddp-2},
     {-0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2},
+    {-0x1.ced7af43cc773p-1, 0x1.b5d1009e15cc0p-2},
     {-0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2},
+    {-0x1.b728345196e3ep-1, 0x1.073879922ffeep-1},
     {-0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1},
+    {-0x1.9b3e047f38741p-1, 0x1.30ff7fce17035p-1},
     {-0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1},
+    {-0x1.7b5df226aafafp-1, 0x1.57d69348ceca0p-1},
     {-0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1},
+    {-0x1.57d69348ceca0p-1, 0x1.7b5df226aafafp-1},
     {-0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1},
+    {-0x1.30ff7fce17035p-1, 0x1.9b3e047f38741p-1},
     {-0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1},
+    {-0x1.073879922ffeep-1, 0x1.b728345196e3ep-1},
     {-0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1},
+    {-0x1.b5d1009e15cc0p-2, 0x1.ced7af43cc773p-1},
     {-0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1},
+    {-0x1.58f9a75ab1fddp-2, 0x1.e212104f686e5p-1},
     {-0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1},
+    {-0x1.f19f97b215f1bp-3, 0x1.f0a7efb9230d7p-1},
     {-0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1},
+    {-0x1.2c8106e8e613ap-3, 0x1.fa7557f08a517p-1},
     {-0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
+    {-0x1.91f65f10dd814p-5, 0x1.ff621e3796d7ep-1},
 };
 
 // Two angles at once: both reductions and both table loads are issued before either pair of
@@ -158,24 +223,19 @@ constexpr double TRIG_TAB[64][2] = {
 CTR_HD void sincos_tab2(double x0, double x1, const double (*tab)[2], double &s0, double &c0, double &s1,
                         double &c1)
 {
-    const double n0 = rint(x0 * 10.185916357881302), n1 = rint(x1 * 10.185916357881302);
-    const int k0 = ((int)n0) & 63, k1 = ((int)n1) & 63;
+    const double n0 = rint(x0 * 20.371832715762604), n1 = rint(x1 * 20.371832715762604);   // round(x 64/pi)
+    const int k0 = ((int)n0) & 127, k1 = ((int)n1) & 127;
     const double ts0 = tab[k0][0], tc0 = tab[k0][1];
     const double ts1 = tab[k1][0], tc1 = tab[k1][1];
-    double r0 = fma(-n0, 0.09817477042468103, x0), r1 = fma(-n1, 0.09817477042468103, x1);
-    r0 = fma(-n0, 3.827021247335479e-18, r0);
-    r1 = fma(-n1, 3.827021247335479e-18, r1);
-    r0 = fma(-n0, -9.358655655369811e-35, r0);
-    r1 = fma(-n1, -9.358655655369811e-35, r1);
+    double r0 = fma(-n0, 0.04908738521234052, x0), r1 = fma(-n1, 0.04908738521234052, x1);
+    r0 = fma(-n0, 1.9135106236677394e-18, r0);
+    r1 = fma(-n1, 1.9135106236677394e-18, r1);
     const double z0 = r0 * r0, z1 = r1 * r1;
-    const double sp0 = fma(z0, fma(z0, fma(z0, 2.7557319223985893e-06, -1.9841269841269841e-04),
-                                   8.3333333333333332e-03), -1.6666666666666666e-01);
-    const double sp1 = fma(z1, fma(z1, fma(z1, 2.7557319223985893e-06, -1.9841269841269841e-04),
-                                   8.3333333333333332e-03), -1.6666666666666666e-01);
-    const double cp0 = fma(z0, fma(z0, fma(z0, 2.4801587301587302e-05, -1.3888888888888889e-03),
-                                   4.1666666666666664e-02), -0.5);
-    const double cp1 = fma(z1, fma(z1, fma(z1, 2.4801587301587302e-05, -1.3888888888888889e-03),
-                                   4.1666666666666664e-02), -0.5);
+    // sin r = r + r z (-1/6 + z (1/120 - z / 5040)),  cos r = 1 + z (-1/2 + z (1/24 - z / 720))
+    const double sp0 = fma(z0, fma(z0, -1.9841269841269841e-04, 8.3333333333333332e-03), -1.6666666666666666e-01);
+    const double sp1 = fma(z1, fma(z1, -1.9841269841269841e-04, 8.3333333333333332e-03), -1.6666666666666666e-01);
+    const double cp0 = fma(z0, fma(z0, -1.3888888888888889e-03, 4.1666666666666664e-02), -0.5);
+    const double cp1 = fma(z1, fma(z1, -1.3888888888888889e-03, 4.1666666666666664e-02), -0.5);
     const double sr0 = fma(r0 * z0, sp0, r0), sr1 = fma(r1 * z1, sp1, r1);
     const double cr0 = fma(z0, cp0, 1.0), cr1 = fma(z1, cp1, 1.0);
     s0 = fma(ts0, cr0, tc0 * sr0);
@@ -186,23 +246,8 @@ CTR_HD void sincos_tab2(double x0, double x1, const double (*tab)[2], double &s0
 
 CTR_HD void sincos_tab(double x, const double (*tab)[2], double &sv, double &cv)
 {
-    const double n = rint(x * 10.185916357881302);            // round(x * 32/pi)
-    double r = fma(-n, 0.09817477042468103, x);                // pi/32 = P1 + P2 + P3 (pi/2 split / 16)
-    r = fma(-n, 3.827021247335479e-18, r);
-    r = fma(-n, -9.358655655369811e-35, r);
-    const int k = ((int)n) & 63;
-    const double z = r * r;
-    // sin r = r + r z (-1/6 + z (1/120 + z (-1/5040 + z / 362880)))      |r| <= 0.0491
-    const double sp = fma(z, fma(z, fma(z, 2.7557319223985893e-06, -1.9841269841269841e-04),
-                                 8.3333333333333332e-03), -1.6666666666666666e-01);
-    const double sr = fma(r * z, sp, r);
-    // cos r = 1 + z (-1/2 + z (1/24 + z (-1/720 + z / 40320)))
-    const double cp = fma(z, fma(z, fma(z, 2.4801587301587302e-05, -1.3888888888888889e-03),
-                                 4.1666666666666664e-02), -0.5);
-    const double cr = fma(z, cp, 1.0);
-    const double ts = tab[k][0], tc = tab[k][1];
-    sv = fma(ts, cr, tc * sr);
-    cv = fma(tc, cr, -(ts * sr));
+    double s1, c1;
+    sincos_tab2(x, 0.0, tab, sv, cv, s1, c1);
 }
 
 CTR_HD void sincos_cw(double x, double *sp, double *cp)
@@ -249,6 +294,20 @@ CTR_HD double rcp1(double x)
 #if defined(__HIP_DEVICE_COMPILE__)
     const double r = __builtin_amdgcn_rcp(x);
     return fma(r, fma(-x, r, 1.0), r);
+#else
+    return 1.0 / x;
+#endif
+}
+
+// 1/x as the bare v_rcp_f64 estimate (relative error <= 2^-24, tools/ubench/rcp_acc: max 2.6e8 ulp).
+// Used only for the 18 error scales 1/(atol + |y| rtol) of the RK45 step controller: the error
+// norm, and from it the accept/reject decision and the next step size, then carry a relative
+// error below 6e-8, which moves h by < 1.2e-8 relative (the tip by ~1e-12 m) and flips an
+// accept/reject decision only when the norm is within 6e-8 of 1.
+CTR_HD double rcp_est(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcp(x);
 #else
     return 1.0 / x;
 #endif
