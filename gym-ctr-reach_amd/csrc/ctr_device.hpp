@@ -387,11 +387,14 @@ struct Stage {
 };
 
 // Full derivative at a state y whose (u_z, R) derivatives are d: builds alpha' and r'.
+// MASKED = false: the caller keeps u_z of absent tubes 1 and 2 at 0 (fk_lane), so alpha'_1,2 = u_z
+// as is; tube 0 is always masked (its u_z drives the frame even where the tube is absent).
+template <bool MASKED = true>
 __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const double *uz, const double *R, Stage &k,
                                          double rcol[3])
 {
     #pragma unroll
-    for (int j = 0; j < 3; ++j) k.al[j] = ((p.present >> j) & 1u) ? uz[j] : 0.0;
+    for (int j = 0; j < 3; ++j) k.al[j] = ((!MASKED && j > 0) || ((p.present >> j) & 1u)) ? uz[j] : 0.0;
     rcol[0] = R[2]; rcol[1] = R[5]; rcol[2] = R[8];
 }
 
@@ -410,6 +413,13 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 
     // state y = [u_z(3), alpha(3), r(3), R(9)]
     double yu[3] = {0.0, 0.0, 0.0};
+    // u_z of an absent tube (EI = 0) has zero derivative and alpha' = 0 there (model.py:97-102).
+    // A tube is present on one contiguous run of segments, so u_z stays 0 before its run; when the
+    // run of tube 1 or 2 ends its value is parked in uzf and the live u_z is zeroed, so
+    // alpha' = u_z needs no mask in the stages.  The parked value only enters select_initial_step's
+    // d0 (common.py:104-106).  Tube 0 keeps its u_z: the frame rotates with u_z,0 even past the
+    // tube's tip (model.py:104-107), which set_action's unchecked nesting pass can produce (Q8).
+    double uzf[3] = {0.0, 0.0, 0.0};
     double ya[3] = {(double)q[3], (double)q[4], (double)q[5]};
     double yr[3] = {0.0, 0.0, 0.0};
     double yR[9];
@@ -447,6 +457,12 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
             p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), RIGID);
+            #pragma unroll
+            for (int j = 1; j < 3; ++j) {
+                const bool absent = !((p.present >> j) & 1u);
+                uzf[j] = (absent && yu[j] != 0.0) ? yu[j] : uzf[j];
+                yu[j] = absent ? 0.0 : yu[j];
+            }
             const double endk = end_lds[k * CTR_BLOCK];
             const double a = prev_end, b = endk - 1e-6;          // model.py:141 linspace endpoints
             const double t0 = fmin(a, b);
@@ -463,7 +479,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             // RungeKutta.__init__: f = fun(t0, y0) -- the trig of y is already known
             rhs_core<HAS_UY>(p, ty, yu, yR, f.uz, f.R);
             double fr[3];
-            stage_at(p, ty, yu, yR, f, fr);
+            stage_at<false>(p, ty, yu, yR, f, fr);
             st.nfev++;
 #ifndef CTR_DIAG_WAVE
             st.nseg++;
@@ -484,10 +500,11 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
                 break;
             }
             // select_initial_step (common.py:68-140), order 4, direction +1
-            double isc_u[3], isc_a[3], isc_r[3], isc_R[9];
+            double isc_u[3], isc_a[3], isc_r[3], isc_R[9], yuref[3];
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                isc_u[i] = ctr_math::rcp_est(ATOL + fabs(yu[i]) * RTOL);
+                yuref[i] = (i == 0 || ((p.present >> i) & 1u)) ? yu[i] : uzf[i];   // the reference's u_z
+                isc_u[i] = ctr_math::rcp_est(ATOL + fabs(yuref[i]) * RTOL);
                 isc_a[i] = ctr_math::rcp_est(ATOL + fabs(ya[i]) * RTOL);
                 isc_r[i] = ctr_math::rcp_est(ATOL + fabs(yr[i]) * RTOL);
             }
@@ -496,7 +513,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             double s0 = 0.0, s1 = 0.0;
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                s0 += (yu[i] * isc_u[i]) * (yu[i] * isc_u[i]) + (ya[i] * isc_a[i]) * (ya[i] * isc_a[i]) +
+                s0 += (yuref[i] * isc_u[i]) * (yuref[i] * isc_u[i]) + (ya[i] * isc_a[i]) * (ya[i] * isc_a[i]) +
                       (yr[i] * isc_r[i]) * (yr[i] * isc_r[i]);
                 s1 += (f.uz[i] * isc_u[i]) * (f.uz[i] * isc_u[i]) + (f.al[i] * isc_a[i]) * (f.al[i] * isc_a[i]) +
                       (fr[i] * isc_r[i]) * (fr[i] * isc_r[i]);
@@ -522,7 +539,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             {
                 const Trig t1 = RIGID ? ty : trig_of<CAREFUL>(a1);
                 rhs_core<HAS_UY>(p, t1, u1, R1, f1.uz, f1.R);
-                stage_at(p, t1, u1, R1, f1, f1r);
+                stage_at<false>(p, t1, u1, R1, f1, f1r);
             }
             st.nfev++;
             double s2 = 0.0;
@@ -598,7 +615,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = EXPR_R;                      \
             const Trig tt = RIGID ? ty : trig_of<CAREFUL>(ai);                                \
             rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
-            stage_at(p, tt, ui, Ri, KOUT, rc);                                                 \
+            stage_at<false>(p, tt, ui, Ri, KOUT, rc);                                          \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
                 br[i] += rc[i] * (BCOEF);                                                      \
                 er[i] += rc[i] * (ECOEF);                                                      \
@@ -645,7 +662,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         double k6r[3];
         const Trig tn = RIGID ? ty : trig_of<CAREFUL>(na);
         rhs_core<HAS_UY>(p, tn, nu, nR, K6.uz, K6.R);
-        stage_at(p, tn, nu, nR, K6, k6r);
+        stage_at<false>(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
         // error norm: RMS of h * (K^T E) / (atol + max(|y|, |y_new|) rtol); |h| factored out
         double en2 = 0.0;
