@@ -208,21 +208,23 @@ def main():
                           device=dev if os.environ.get("CTR_BENCH_BACKEND", "nccl") == "nccl" else "cpu")
     total_steps = n * ws * args.steps
 
-    # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset
+    # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset.
+    # ctr_step with autoreset = 0 launches exactly one kernel (k_step) on `stream`; one event pair
+    # brackets k_iters back-to-back launches (per-launch event pairs add their own few us), so the
+    # average includes the ~1.5 us launch boundaries and slightly over-states the kernel time.
     j_probe = env.joints.clone()
     flops_env_step, sincos, nfev_mean = fk_work(env, j_probe)
-    # ctr_step with autoreset = 0 launches exactly one kernel (k_step) on `stream`
     from ctr_reach_amd import _abi
-    k_iters = max(5, min(args.steps, 20))
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k_iters)]
+    k_iters = max(5, min(args.steps, 32))
     sp = _abi.stream_ptr(stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
     for i in range(k_iters):
-        ev[i][0].record(stream)
         rc = env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[i % len(acts)]), env._out, 0, sp)
-        ev[i][1].record(stream)
         _abi.check(rc, "ctr_step")
+    e1.record(stream)
     torch.cuda.synchronize()
-    k_ms = sum(a.elapsed_time(b) for a, b in ev) / k_iters
+    k_ms = e0.elapsed_time(e1) / k_iters
 
     if rank != 0:
         if dist:

@@ -26,6 +26,12 @@ __global__ __launch_bounds__(256) void kern(double *out, unsigned long long *cyc
         if (OP == 8) { a = ctr_math::rcp1(a) + 0.5; b = ctr_math::rcp1(b) + 0.5; c = ctr_math::rcp1(c) + 0.5; d = ctr_math::rcp1(d) + 0.5; }
         if (OP == 9) { a = ctr_math::powpos(a, -0.2) + 0.5; b = ctr_math::powpos(b, -0.2) + 0.5; c = ctr_math::powpos(c, -0.2) + 0.5; d = ctr_math::powpos(d, -0.2) + 0.5; }
         if (OP == 10) { a = __builtin_amdgcn_rsq(a) + 0.5; b = __builtin_amdgcn_rsq(b) + 0.5; c = __builtin_amdgcn_rsq(c) + 0.5; d = __builtin_amdgcn_rsq(d) + 0.5; }
+        if (OP == 12) { a = rint(a) + 0.37; b = rint(b) + 0.37; c = rint(c) + 0.37; d = rint(d) + 0.37; }
+        if (OP == 13) { a = (double)(int)a + 0.37; b = (double)(int)b + 0.37; c = (double)(int)c + 0.37; d = (double)(int)d + 0.37; }
+        if (OP == 14) { a = (double)(float)a + 0.37; b = (double)(float)b + 0.37; c = (double)(float)c + 0.37; d = (double)(float)d + 0.37; }
+        if (OP == 15) { a = fmax(a, 0.3) + 0.37; b = fmax(b, 0.3) + 0.37; c = fmax(c, 0.3) + 0.37; d = fmax(d, 0.3) + 0.37; }
+        if (OP == 16) { a = (a + 6755399441055744.0) - 6755399441055744.0 + 0.37; b = (b + 6755399441055744.0) - 6755399441055744.0 + 0.37;
+                        c = (c + 6755399441055744.0) - 6755399441055744.0 + 0.37; d = (d + 6755399441055744.0) - 6755399441055744.0 + 0.37; }
         if (OP == 11) { a = (double)__builtin_amdgcn_rcpf((float)a) + 0.5; b = (double)__builtin_amdgcn_rcpf((float)b) + 0.5; c = (double)__builtin_amdgcn_rcpf((float)c) + 0.5; d = (double)__builtin_amdgcn_rcpf((float)d) + 0.5; }
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -54,6 +60,11 @@ int main()
     hipMalloc(&out, 256 * 256 * sizeof(double));
     hipMalloc(&cyc, 256 * sizeof(unsigned long long));
     run<0>("v_fma_f64", out, cyc);
+    run<12>("v_rndne_f64 (+add)", out, cyc);
+    run<13>("cvt f64->i32->f64 (+add)", out, cyc);
+    run<14>("cvt f64->f32->f64 (+add)", out, cyc);
+    run<15>("v_max_f64 (+add)", out, cyc);
+    run<16>("2 adds (magic round) (+add)", out, cyc);
     run<1>("v_rcp_f64 (+add)", out, cyc);
     run<8>("rcp1 (rcp+2fma)(+add)", out, cyc);
     run<11>("f32 rcp via cvt (+add)", out, cyc);
