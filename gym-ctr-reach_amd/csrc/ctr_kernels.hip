@@ -13,6 +13,7 @@
 //   k_fk_shape    FK + backbone shape r at 30 dense-output points/segment (envs/model.py:66-68,119-174)
 //   k_jacobian    forward-difference tip Jacobian, 7 lanes per env       (CTR_Python/CTR_Model.py:251-262)
 //   k_domain_params  each env's current (domain-randomised) tube table  (envs/model.py:20-28)
+//   k_her_*       HER replay feed: episode recording, relabelled uniform sampling (ctr_her.inc)
 //
 // Work lists (auto-reset misses, pool refills) are appended with one wave-aggregated atomic per
 // wave.  The tube tables (<= 8 systems x 18 doubles) travel as a kernel argument and are staged
@@ -832,3 +833,5 @@ int ctr_compute_reward(const double *achieved, const double *desired, int64_t n,
 }
 
 }  // extern "C"
+
+#include "ctr_her.inc"

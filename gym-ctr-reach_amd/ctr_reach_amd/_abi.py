@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 5
+CTR_ABI_VERSION = 6
 CTR_MAX_SYSTEMS = 8
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1
@@ -19,6 +19,9 @@ CTR_MODEL_RIGID = 1
 CTR_STATUS_STEP_UNDERFLOW = 1
 CTR_STATUS_SAMPLER_STUCK = 2
 CTR_STATUS_NAN = 4
+CTR_HER_FUTURE = 0
+CTR_HER_FINAL = 1
+CTR_HER_EPISODE = 2
 
 _d3 = ctypes.c_double * 3
 _P = ctypes.c_void_p
@@ -97,8 +100,37 @@ class CtrStepOut(ctypes.Structure):
     ]
 
 
+class CtrHer(ctypes.Structure):
+    _fields_ = [
+        ("obs_dim", ctypes.c_int32),
+        ("t_max", ctypes.c_int32),
+        ("n_sampled_goal", ctypes.c_int32),
+        ("strategy", ctypes.c_int32),
+        ("n", ctypes.c_int64),
+        ("env_base", ctypes.c_int64),
+        ("slots", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("obs", _P),
+        ("ag", _P),
+        ("action", _P),
+        ("reward", _P),
+        ("dg", _P),
+        ("tol", _P),
+        ("len", _P),
+        ("epoch", _P),
+        ("cur_t", _P),
+        ("cur_epoch", _P),
+    ]
+
+
+class CtrHerBatch(ctypes.Structure):
+    _fields_ = [("obs", _P), ("action", _P), ("reward", _P), ("next_obs", _P), ("done", _P), ("index", _P)]
+
+
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
-            "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape")
+            "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
+            "ctr_her_open", "ctr_her_record", "ctr_her_sample")
 
 _lib = None
 
@@ -130,8 +162,14 @@ def load(path=None):
     L.ctr_fk_tables.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), _P, _P, _P, _P]
     L.ctr_fk_shape.argtypes = [_P, _P, _P, i64, ctypes.POINTER(CtrEnvConfig), i32, _P, _P, _P, _P, _P, _P]
     L.ctr_jacobian.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), ctypes.c_double, _P, _P, _P, _P]
+    L.ctr_her_open.argtypes = [ctypes.POINTER(CtrHer), ctypes.POINTER(CtrBatch), _P, _P, _P]
+    L.ctr_her_record.argtypes = [ctypes.POINTER(CtrHer), ctypes.POINTER(CtrBatch), _P, ctypes.POINTER(CtrStepOut),
+                                 ctypes.c_double, _P]
+    L.ctr_her_sample.argtypes = [ctypes.POINTER(CtrHer), i64, ctypes.c_uint64, ctypes.c_uint64,
+                                 ctypes.POINTER(CtrHerBatch), _P]
     for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward",
-               "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape"):
+               "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
+               "ctr_her_open", "ctr_her_record", "ctr_her_sample"):
         getattr(L, fn).restype = ctypes.c_int
     if L.ctr_abi_version() != CTR_ABI_VERSION:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))

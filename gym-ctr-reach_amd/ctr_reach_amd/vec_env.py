@@ -173,6 +173,7 @@ class CtrReachVecEnv(object):
             self.refill_cap = 0
         self._batch = _abi.CtrBatch()
         self._out = _abi.CtrStepOut()
+        self._her = None          # HerReplayBuffer bound by enable_her()
         self._fill_structs()
 
     # ------------------------------------------------------------------ plumbing
@@ -199,6 +200,13 @@ class CtrReachVecEnv(object):
         torch = _torch()
         self.nfev = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device) if on else None
         self._fill_structs()
+
+    def enable_her(self, slots=4, n_sampled_goal=4, goal_selection_strategy="future", seed=None):
+        """Bind a device HER replay feed (ctr_reach_amd.her.HerReplayBuffer): every later reset /
+        step records into it.  Call before reset()."""
+        from .her import HerReplayBuffer
+        return HerReplayBuffer(self, slots=slots, n_sampled_goal=n_sampled_goal,
+                               goal_selection_strategy=goal_selection_strategy, seed=seed)
 
     def _obs_dict(self):
         return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
@@ -239,6 +247,8 @@ class CtrReachVecEnv(object):
         rc = self.lib.ctr_reset(self.cfg, self._batch, _abi.ptr(m), _abi.ptr(g), _abi.ptr(s), _abi.ptr(self.obs),
                                 _abi.ptr(self.status), _abi.stream_ptr(stream))
         _abi.check(rc, "ctr_reset")
+        if self._her is not None:
+            self._her._open(m, stream)
         self.refill_pool(stream)
         return self._obs_dict()
 
@@ -265,6 +275,8 @@ class CtrReachVecEnv(object):
                                _abi.stream_ptr(stream))
         if rc:
             _abi.check(rc, "ctr_step")
+        if self._her is not None:
+            self._her._record(actions, stream)
         if self.autoreset:
             self._batch.work_parity ^= 1
         if self.pool_depth:

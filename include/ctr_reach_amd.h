@@ -29,6 +29,13 @@
  *   ctr_jacobian        CTR_Model.jac (finite differences)             envs/CTR_Python/CTR_Model.py:251-262
  *   ctr_domain_params   Model.current_sys_parameters after randomize_parameters
  *                                                                          envs/model.py:20-28, model_utils.py:5-35
+ *   ctr_her_open / ctr_her_record / ctr_her_sample
+ *                       the replay side of the reference's training pipeline: stable-baselines 2
+ *                       HER (HindsightExperienceReplayWrapper.add / _store_episode /
+ *                       _sample_achieved_goal, ReplayBuffer.sample) with the reference's
+ *                       settings goal_selection_strategy 'future', n_sampled_goal 4
+ *                       (saved_policies/.../her/CTR-Generic-Reach-v0_1/CTR-Generic-Reach-v0/
+ *                       config.yml), fed by CtrReachEnv.compute_reward (ctr_reach_env.py:160-170)
  */
 #ifndef CTR_REACH_AMD_H
 #define CTR_REACH_AMD_H
@@ -39,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 5
+#define CTR_ABI_VERSION 6
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -149,6 +156,82 @@ typedef struct ctr_step_out_t {
     uint32_t *status;            /* [n] or NULL: CTR_STATUS_* bits                               */
     uint32_t *nfev;              /* [n] or NULL: RHS evaluations spent in the step's FK          */
 } ctr_step_out_t;
+
+/* ---------------------------------------------------------------------------------------
+ * HER replay feed (device).  Episodes are recorded where the environments run and relabelled
+ * with stable-baselines 2 HER semantics:
+ *   - an episode enters the replay store when it ends (HindsightExperienceReplayWrapper.add
+ *     stores on done); its L transitions become L real rows plus, per transition t, k relabelled
+ *     rows (FUTURE: none for the last transition), in _store_episode's order;
+ *   - a relabelled row of transition t takes the achieved goal of obs_sel, the observation
+ *     before transition sel (_sample_achieved_goal returns selected_transition[0]'s
+ *     achieved_goal): FUTURE sel ~ U{t+1 .. L-1}, FINAL sel = L-1, EPISODE sel ~ U{0 .. L-1};
+ *     its reward is compute_reward(achieved goal of obs_{t+1}, goal) at the tolerance in force
+ *     when the episode ended, its done is 0; only the desired_goal slots change (the
+ *     'observation' part, which holds dg - ag, is kept, as the wrapper keeps it);
+ *   - ctr_her_sample draws rows uniformly with replacement over all stored rows
+ *     (ReplayBuffer.sample) and returns them in HERGoalEnvWrapper's flat layout
+ *     [observation, achieved_goal, desired_goal].
+ * Storage: each environment owns `slots` episode slots used round-robin (slot of episode r of
+ * env e = e * slots + r mod slots), so the store keeps each env's last slots - 1 finished
+ * episodes (first-in first-out per env; stable-baselines drops the globally oldest rows).
+ * The sel draws are a pure function of (seed, global env id, reset number, t, j) (Philox
+ * stream 4): they are fixed per row, as the wrapper fixes them when it stores the episode. */
+#define CTR_HER_FUTURE  0
+#define CTR_HER_FINAL   1
+#define CTR_HER_EPISODE 2
+
+typedef struct ctr_her_t {
+    int32_t  obs_dim;          /* 13 or 14                                                  */
+    int32_t  t_max;            /* longest episode (max_steps_per_episode), <= 65535          */
+    int32_t  n_sampled_goal;   /* k (4), <= 255                                              */
+    int32_t  strategy;         /* CTR_HER_*                                                  */
+    int64_t  n;                /* environments                                               */
+    int64_t  env_base;         /* global id of environment 0 (keys the relabel draws)       */
+    int32_t  slots;            /* episode slots per environment (>= 2)                      */
+    int32_t  pad;
+    uint64_t seed;             /* Philox key of the relabel draws                            */
+    /* episode store, E = n * slots slots (device) */
+    float    *obs;             /* [E][t_max + 1][obs_dim]  obs_0 .. obs_L                    */
+    double   *ag;              /* [E][t_max + 1][3]        achieved goal of obs_t            */
+    float    *action;          /* [E][t_max][6]                                              */
+    float    *reward;          /* [E][t_max]                                                 */
+    double   *dg;              /* [E][3]                   the episode's desired goal         */
+    double   *tol;             /* [E]                      tolerance when the episode ended   */
+    int32_t  *len;             /* [E]   L of a stored episode; 0 = empty, -1 = being recorded */
+    uint32_t *epoch;           /* [E]   reset number of the episode in the slot              */
+    /* per environment (device) */
+    int32_t  *cur_t;           /* [n]   transitions recorded in the open episode; -1 = none  */
+    uint32_t *cur_epoch;       /* [n]   reset number of the open episode                     */
+} ctr_her_t;
+
+/* Flat sampled batch (device), d = obs_dim + 6. */
+typedef struct ctr_her_batch_t {
+    float   *obs;              /* [B][d]  [observation_t, achieved_goal_t, desired_goal]      */
+    float   *action;           /* [B][6]                                                      */
+    float   *reward;           /* [B]                                                         */
+    float   *next_obs;         /* [B][d]  [observation_t+1, achieved_goal_t+1, desired_goal]  */
+    float   *done;             /* [B]     1 for the last real transition of an episode        */
+    int32_t *index;            /* [B][3] or NULL: (slot, t, j), j = 0 real, 1..k relabelled;
+                                  slot -1: no stored row found in 256 draws                  */
+} ctr_her_batch_t;
+
+/* Opens an episode for the environments with mask[i] != 0 (NULL = all) from the batch's
+ * current state (after ctr_reset): obs_0 = obs [n][obs_dim], its achieved goal, the desired
+ * goal and the reset number.  An episode still open in that env is discarded. */
+int ctr_her_open(const ctr_her_t *her, const ctr_batch_t *batch, const float *obs, const uint8_t *mask,
+                 void *stream);
+
+/* Records the step that ctr_step (autoreset on) just made: action [n][6], out's reward / done /
+ * obs / terminal_obs / terminal_achieved (terminal_* required).  A done env's episode is closed
+ * with the tolerance tol and stored; the env's next episode is opened from the post-reset
+ * state. */
+int ctr_her_record(const ctr_her_t *her, const ctr_batch_t *batch, const float *actions,
+                   const ctr_step_out_t *out, double tol, void *stream);
+
+/* Draws B rows uniformly over the stored rows; draws are keyed (seed, counter, row). */
+int ctr_her_sample(const ctr_her_t *her, int64_t batch_size, uint64_t seed, uint64_t counter,
+                   const ctr_her_batch_t *out, void *stream);
 
 int ctr_abi_version(void);
 const char *ctr_last_error(void);

@@ -52,7 +52,7 @@ def test_struct_layout_matches_header(tmp_path):
     from ctr_reach_amd import _abi
     structs = [(_abi.CtrSystem, "ctr_system_t"), (_abi.CtrTubeRaw, "ctr_tube_raw_t"),
                (_abi.CtrEnvConfig, "ctr_env_config_t"), (_abi.CtrBatch, "ctr_batch_t"),
-               (_abi.CtrStepOut, "ctr_step_out_t")]
+               (_abi.CtrStepOut, "ctr_step_out_t"), (_abi.CtrHer, "ctr_her_t"), (_abi.CtrHerBatch, "ctr_her_batch_t")]
     lines, want = [], []
     for cls, cname in structs:
         lines.append('  printf("%%zu\\n", sizeof(%s));' % cname)
@@ -168,3 +168,19 @@ def test_solver_kwargs_validation():
         solver_codes("euler", 10, "compliant")
     with pytest.raises(ValueError):
         solver_codes("rk45_scipy", 0, "stiff")
+
+
+def test_her_abi_rejects_bad_arguments_without_gpu():
+    from ctr_reach_amd import _abi
+    lib = _abi.load()
+    h = _abi.CtrHer()
+    h.obs_dim, h.t_max, h.n_sampled_goal, h.strategy, h.slots, h.n = 13, 150, 4, 0, 4, 0
+    b = _abi.CtrBatch()
+    assert lib.ctr_her_open(h, b, ctypes.c_void_p(1), None, None) == 0          # empty store: no-op
+    h.slots = 1
+    assert lib.ctr_her_open(h, b, ctypes.c_void_p(1), None, None) == -1 and b"slots" in lib.ctr_last_error()
+    h.slots, h.strategy = 4, 7
+    assert lib.ctr_her_record(h, b, ctypes.c_void_p(1), _abi.CtrStepOut(), 0.02, None) == -1
+    h.strategy, h.n = 0, 8
+    assert lib.ctr_her_sample(h, 4, 0, 0, _abi.CtrHerBatch(), None) == -1 and b"buffer" in lib.ctr_last_error()
+    assert lib.ctr_her_sample(None, 4, 0, 0, _abi.CtrHerBatch(), None) == -1
