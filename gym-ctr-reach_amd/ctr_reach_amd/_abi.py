@@ -111,10 +111,8 @@ class CtrHer(ctypes.Structure):
         ("slots", ctypes.c_int32),
         ("pad", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
-        ("obs", _P),
-        ("ag", _P),
-        ("action", _P),
-        ("reward", _P),
+        ("state", _P),
+        ("step", _P),
         ("dg", _P),
         ("tol", _P),
         ("len", _P),

@@ -50,10 +50,13 @@ class HerReplayBuffer(object):
         n, dev, T = venv.num_envs, venv.device, self.t_max
         E = n * self.slots
         f32, f64, i32 = torch.float32, torch.float64, torch.int32
-        self.obs = torch.zeros((E, T + 1, self.obs_dim), dtype=f32, device=dev)
-        self.ag = torch.zeros((E, T + 1, 3), dtype=f64, device=dev)
-        self.action = torch.zeros((E, T, 6), dtype=f32, device=dev)
-        self.reward = torch.zeros((E, T), dtype=f32, device=dev)
+        S = self.slots                     # env-minor 96-B / 32-B rows (include/ctr_reach_amd.h ctr_her_t)
+        self.state = torch.zeros((S, T + 1, n, 24), dtype=f32, device=dev)
+        self.step_rows = torch.zeros((S, T, n, 8), dtype=f32, device=dev)
+        self.obs = self.state[..., :self.obs_dim]                       # views
+        self.ag = self.state[..., 16:22].view(f64)
+        self.action = self.step_rows[..., :6]
+        self.reward = self.step_rows[..., 6]
         self.dg = torch.zeros((E, 3), dtype=f64, device=dev)
         self.tol = torch.zeros(E, dtype=f64, device=dev)
         self.len = torch.zeros(E, dtype=i32, device=dev)
@@ -64,7 +67,7 @@ class HerReplayBuffer(object):
         h = self._h = _abi.CtrHer()
         h.obs_dim, h.t_max, h.n_sampled_goal, h.strategy = self.obs_dim, T, self.n_sampled_goal, STRATEGIES[self.strategy]
         h.n, h.env_base, h.slots, h.seed = n, venv.env_base, self.slots, self.seed
-        h.obs, h.ag, h.action, h.reward = p(self.obs), p(self.ag), p(self.action), p(self.reward)
+        h.state, h.step = p(self.state), p(self.step_rows)
         h.dg, h.tol, h.len, h.epoch = p(self.dg), p(self.tol), p(self.len), p(self.epoch)
         h.cur_t, h.cur_epoch = p(self.cur_t), p(self.cur_epoch)
         self._counter = 0
@@ -72,7 +75,7 @@ class HerReplayBuffer(object):
 
     @property
     def nbytes(self):
-        return sum(t.numel() * t.element_size() for t in (self.obs, self.ag, self.action, self.reward, self.dg, self.tol,
+        return sum(t.numel() * t.element_size() for t in (self.state, self.step_rows, self.dg, self.tol,
                                                            self.len, self.epoch, self.cur_t, self.cur_epoch))
 
     # called by CtrReachVecEnv

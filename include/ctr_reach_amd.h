@@ -192,10 +192,13 @@ typedef struct ctr_her_t {
     int32_t  pad;
     uint64_t seed;             /* Philox key of the relabel draws                            */
     /* episode store, E = n * slots slots (device) */
-    float    *obs;             /* [E][t_max + 1][obs_dim]  obs_0 .. obs_L                    */
-    double   *ag;              /* [E][t_max + 1][3]        achieved goal of obs_t            */
-    float    *action;          /* [E][t_max][6]                                              */
-    float    *reward;          /* [E][t_max]                                                 */
+    /* slot id = env * slots + s.  Rows are env-minor ([slots][t][n]) so the lanes of a wave,
+     * consecutive envs mostly at the same (slot, t), write one contiguous span, and 16-B
+     * aligned so every row is whole dwordx4 stores; a sampled row is one or two cache lines. */
+    float    *state;           /* [slots][t_max + 1][n][24], 96-B rows: floats 0 .. obs_dim-1 =
+                                  obs_t (obs_0 .. obs_L), floats 16 .. 21 = its achieved goal
+                                  as 3 doubles                                                */
+    float    *step;            /* [slots][t_max][n][8], 32-B rows: action 0..5, reward 6      */
     double   *dg;              /* [E][3]                   the episode's desired goal         */
     double   *tol;             /* [E]                      tolerance when the episode ended   */
     int32_t  *len;             /* [E]   L of a stored episode; 0 = empty, -1 = being recorded */
