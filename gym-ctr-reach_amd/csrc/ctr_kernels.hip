@@ -472,9 +472,15 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int s_count;
-    if (threadIdx.x == 0) {
-        s_count = (mode == 0) ? min(*miss_counter(b), (int32_t)b.n) : 0;
-        if (mode == 0 && blockIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;   // next step's counter
+    if (mode == 0) {
+        // launched after every auto-reset step; with the reset pool the miss list is almost always
+        // empty, so leave before staging the tables (the launch then costs ~1.5 us, not ~4.7)
+        const int32_t c = min(*miss_counter(b), (int32_t)b.n);
+        if (threadIdx.x == 0 && blockIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;   // next step's counter
+        if (c == 0) return;                              // block-uniform: no barrier is skipped
+        if (threadIdx.x == 0) s_count = c;
+    } else if (threadIdx.x == 0) {
+        s_count = 0;
     }
     stage_systems(kc, s_sys, s_raw);
     const int64_t stride = (mode == 0) ? (int64_t)gridDim.x * (BLOCK / 2) : (int64_t)1 << 62;
