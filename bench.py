@@ -256,7 +256,10 @@ def main():
                      "flops_per_launch": flops_env_step, "sincos_per_launch": sincos,
                      "nfev_per_env_step": nfev_mean,
                      "hbm_gbs_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9,
-                     "hbm_frac_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9 / PEAK_HBM},
+                     "hbm_frac_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9 / PEAK_HBM,
+                     "note": "bound is the FP64 vector pipe: an adaptive RK45 ODE per lane, no GEMM-shaped work for "
+                             "MFMA, ~140 flop/B so HBM is not the limit; peak = MI355X FP64 vector spec; flops = "
+                             "SURVEY 8(d) count from device counters (sincos not priced)"},
     }
     tr = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tr):
@@ -264,6 +267,7 @@ def main():
             t = json.load(fh)
         if t.get("envs") == n and t.get("config", 3) == args.config:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
+            out["roofline"]["traffic_source"] = "profiles/traffic.json: rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE per k_step"
     if not args.no_cpu_baseline and ws == 1:
         out["parity"] = parity_probe(env, cfgd)
         out["cpu_baseline"] = cpu_baseline(args, cfgd)
