@@ -28,6 +28,7 @@ Outputs (all seeded, deterministic):
                   recorded FK outputs) with a per-row flag for whether today's reference
                   reproduces them to 1e-12
   systems.json    the registration tube tables (ctr_reach_envs/__init__.py:7-70)
+  sampler.npz     Obs.sample_goal draws per system (joints f32[4,n,6], candidates tried i32[4,n])
 
 Usage:  python tests/golden/make_golden.py  [--quick]
 """
@@ -400,6 +401,33 @@ def gen_backbone(CtrReachEnv, kwargs, per_sys, max_pts=270):
     print("backbone", len(Q), "max points", max(NPT))
 
 
+def gen_sampler(CtrReachEnv, kwargs, per_sys):
+    """Obs.sample_goal (obs.py:185-207) draws of the reference: the sampled joints and the number
+    of candidates each took (the reference's own numpy RNG, seeded per system)."""
+    env = make_env(CtrReachEnv, kwargs, select_systems=[0, 1, 2, 3])
+    J, T = [], []
+    for s in range(4):
+        box = env.trig_obj.joint_sample_spaces[s]
+        box.np_random = np.random.RandomState(1234 + s)
+        calls = [0]
+        orig = box.sample
+
+        def counting_sample(orig=orig):
+            calls[0] += 1
+            return orig()
+
+        box.sample = counting_sample
+        js, ts = [], []
+        for _ in range(per_sys):
+            calls[0] = 0
+            js.append(np.asarray(env.trig_obj.sample_goal(s), np.float32))
+            ts.append(calls[0])
+        box.sample = orig
+        J.append(js)
+        T.append(ts)
+    np.savez_compressed(os.path.join(OUT, "sampler.npz"), joints=np.array(J, np.float32), tries=np.array(T, np.int32))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -411,6 +439,8 @@ def main():
             gen_jacobian(CtrReachEnv, kwargs, 4 if args.quick else 32)
         if "backbone" in args.only:
             gen_backbone(CtrReachEnv, kwargs, 4 if args.quick else 16)
+        if "sampler" in args.only:
+            gen_sampler(CtrReachEnv, kwargs, 400 if args.quick else 4000)
         return
     sysj = {}
     for s in range(4):
@@ -428,6 +458,7 @@ def main():
     gen_csv_known(CtrReachEnv, kwargs, 2 if args.quick else 25)
     gen_jacobian(CtrReachEnv, kwargs, 4 if args.quick else 32)
     gen_backbone(CtrReachEnv, kwargs, 4 if args.quick else 16)
+    gen_sampler(CtrReachEnv, kwargs, 400 if args.quick else 4000)
 
 
 if __name__ == "__main__":
