@@ -665,19 +665,24 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         stage_at<false>(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
         // error norm: RMS of h * (K^T E) / (atol + max(|y|, |y_new|) rtol); |h| factored out
-        double en2 = 0.0;
+        // three independent partial sums: one wave per SIMD exposes the FMA latency of a single
+        // 18-long accumulation chain at the end of the attempt, where little else can issue
+        double acc[3] = {0.0, 0.0, 0.0};
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yu[i], nu[i]), RTOL, ATOL));
             const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(ya[i], na[i]), RTOL, ATOL));
             const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yr[i], nr[i]), RTOL, ATOL));
-            en2 = fma(xu, xu, fma(xa, xa, fma(xr, xr, en2)));
+            acc[0] = fma(xu, xu, acc[0]);
+            acc[1] = fma(xa, xa, acc[1]);
+            acc[2] = fma(xr, xr, acc[2]);
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
             const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yR[i], nR[i]), RTOL, ATOL));
-            en2 = fma(xR, xR, en2);
+            acc[i / 3] = fma(xR, xR, acc[i / 3]);
         }
+        double en2 = (acc[0] + acc[1]) + acc[2];
         en2 *= h * h;                       // = 18 error_norm^2
         const double en2n = en2 * (1.0 / 18);   // error_norm^2
         // error_norm ** -0.2 = (error_norm^2) ** -0.1
