@@ -264,3 +264,26 @@ def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
         for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs", "terminal_obs"):
             np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(), err_msg=k)
     assert (a.epoch.cpu().numpy() >= 4).all()
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 257])
+def test_ragged_batch_sizes_step_vs_oracle(cuda, oracle_mod, n):
+    """Batches that are not a multiple of a wave (64) or a workgroup (256): every env's step
+    (joints bit-exact, tip <= 1e-10 m, reward bit-exact) against the oracle, 5 steps."""
+    import torch
+    env = _env(cuda, n, seed=11 + n)
+    env.reset()
+    rng = np.random.default_rng(n)
+    for _ in range(5):
+        q0 = env.joints.cpu().numpy().copy()
+        dg = env.desired_goal.cpu().numpy().copy()
+        t0 = env.t.cpu().numpy().copy()
+        act = (rng.uniform(-1, 1, (n, 6)) * env.action_space.high).astype(np.float32)
+        obs, rew, done, info = env.step(torch.tensor(act, device=cuda))
+        torch.cuda.synchronize()
+        d = done.cpu().numpy()
+        ref = oracle_mod.step(q0, act, dg, t0, env.get_goal_tolerance())
+        keep = ~d                                    # done envs were auto-reset (checked elsewhere)
+        np.testing.assert_array_equal(env.joints.cpu().numpy()[keep], ref["joints"][keep])
+        assert np.abs(env.achieved_goal.cpu().numpy()[keep] - ref["achieved_goal"][keep]).max(initial=0.0) < 1e-10
+        np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"].astype(np.float32))
