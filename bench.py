@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--profile-only", action="store_true", help="no timing extras (for rocprofv3)")
     ap.add_argument("--refill-interval", type=int, default=None, help="reset-pool refill interval (steps)")
+    ap.add_argument("--systems", default="0",
+                    help="select_systems, comma-separated registration indices (default 0, the headline; "
+                         "'0,1,2,3' is SURVEY.md 8(d)'s mixed-system divergence check)")
     return ap.parse_args()
 
 
@@ -123,8 +126,8 @@ def parity_probe(env, cfgd):
     sysid = env.system.detach().cpu().numpy()
     dg = env.desired_goal.detach().cpu().numpy()
     tip = env.forward_kinematics(env.joints, env.system).cpu().numpy()
-    ref = oracle.fk(q, sysid, integrator=cfgd["integrator"], steps_per_m=cfgd["rk4_steps_per_m"],
-                    model=cfgd["model"])["tip"]
+    ref = oracle.fk(q, sysid, systems=oracle.make_systems(select=env.select_systems), integrator=cfgd["integrator"],
+                    steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"])["tip"]
     l2 = np.linalg.norm(tip - ref, axis=1)
     tol = env.goal_tolerance.get_tol()
     d_gpu = np.linalg.norm(tip - dg, axis=1)
@@ -178,9 +181,10 @@ def main():
     cfgd = CONFIGS[args.config]
     n = args.envs or cfgd["envs"]
     extra = {} if args.refill_interval is None else {"refill_interval": args.refill_interval}
+    systems = [int(s) for s in args.systems.split(",")]
     env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
                          integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"],
-                         **extra)
+                         select_systems=systems, **extra)
     env.reset()
     acts = make_actions(env, 8, args.seed + rank)
     stream = torch.cuda.current_stream()
@@ -244,8 +248,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: Philox-sampled joints/goals (sample_goal region), uniform actions in the action box",
-        "config": {"workload": (cfgd["text"] % n) + ", system 0, n_substeps 10, tol 0.020, max 150 steps, "
-                                                     "auto-reset",
+        "config": {"workload": (cfgd["text"] % n) + ", %s, n_substeps 10, tol 0.020, max 150 steps, "
+                                                     "auto-reset" % ("system %d" % systems[0] if len(systems) == 1 else
+                                                                     "systems %s drawn per reset" % args.systems),
                    "integrator": cfgd["integrator"], "model": cfgd["model"],
                    "rk4_steps_per_m": cfgd["rk4_steps_per_m"] if cfgd["integrator"] == "rk4" else None,
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
@@ -265,7 +270,7 @@ def main():
     if os.path.exists(tr):
         with open(tr) as fh:
             t = json.load(fh)
-        if t.get("envs") == n and t.get("config", 3) == args.config:
+        if t.get("envs") == n and t.get("config", 3) == args.config and systems == [0]:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
             out["roofline"]["traffic_source"] = "profiles/traffic.json: rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE per k_step"
     if not args.no_cpu_baseline and ws == 1:

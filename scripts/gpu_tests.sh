@@ -14,3 +14,4 @@ run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 400 python bench.py --steps 20 --warmup 5 --cpu-seconds 5
 run bench_c2 300 python bench.py --config 2 --steps 20 --warmup 5 --cpu-seconds 5
 run bench_c5 300 python bench.py --config 5 --steps 20 --warmup 5 --cpu-seconds 5
+run bench_mixed 300 python bench.py --systems 0,1,2,3 --steps 20 --warmup 5 --cpu-seconds 5
