@@ -10,8 +10,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 6
+CTR_ABI_VERSION = 7
 CTR_MAX_SYSTEMS = 8
+CTR_HER_SCAN_TILE = 1024
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1
 CTR_MODEL_COMPLIANT = 0
@@ -119,6 +120,7 @@ class CtrHer(ctypes.Structure):
         ("epoch", _P),
         ("cur_t", _P),
         ("cur_epoch", _P),
+        ("cdf", _P),
     ]
 
 

@@ -63,20 +63,23 @@ class HerReplayBuffer(object):
         self.epoch = torch.zeros(E, dtype=i32, device=dev)
         self.cur_t = torch.full((n,), -1, dtype=i32, device=dev)
         self.cur_epoch = torch.zeros(n, dtype=i32, device=dev)
+        tile = _abi.CTR_HER_SCAN_TILE        # sampler scratch: CTR_HER_CDF_LEN(E) prefix sums
+        self.cdf = torch.zeros(E + (E + tile - 1) // tile + 1, dtype=torch.int64, device=dev)
         p = _abi.ptr
         h = self._h = _abi.CtrHer()
         h.obs_dim, h.t_max, h.n_sampled_goal, h.strategy = self.obs_dim, T, self.n_sampled_goal, STRATEGIES[self.strategy]
         h.n, h.env_base, h.slots, h.seed = n, venv.env_base, self.slots, self.seed
         h.state, h.step = p(self.state), p(self.step_rows)
         h.dg, h.tol, h.len, h.epoch = p(self.dg), p(self.tol), p(self.len), p(self.epoch)
-        h.cur_t, h.cur_epoch = p(self.cur_t), p(self.cur_epoch)
+        h.cur_t, h.cur_epoch, h.cdf = p(self.cur_t), p(self.cur_epoch), p(self.cdf)
         self._counter = 0
         venv._her = self
 
     @property
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (self.state, self.step_rows, self.dg, self.tol,
-                                                           self.len, self.epoch, self.cur_t, self.cur_epoch))
+                                                           self.len, self.epoch, self.cur_t, self.cur_epoch,
+                                                           self.cdf))
 
     # called by CtrReachVecEnv
     def _open(self, mask, stream):

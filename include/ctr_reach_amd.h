@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 6
+#define CTR_ABI_VERSION 7
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -206,7 +206,13 @@ typedef struct ctr_her_t {
     /* per environment (device) */
     int32_t  *cur_t;           /* [n]   transitions recorded in the open episode; -1 = none  */
     uint32_t *cur_epoch;       /* [n]   reset number of the open episode                     */
+    /* sampler scratch (device), CTR_HER_CDF_LEN(n * slots) int64: every ctr_her_sample call
+     * rebuilds the prefix sums of the stored rows per slot here, so a draw is one search */
+    int64_t  *cdf;
 } ctr_her_t;
+
+#define CTR_HER_SCAN_TILE 1024     /* slots per scan tile of the sampler's prefix sums */
+#define CTR_HER_CDF_LEN(E) ((E) + ((E) + CTR_HER_SCAN_TILE - 1) / CTR_HER_SCAN_TILE + 1)
 
 /* Flat sampled batch (device), d = obs_dim + 6. */
 typedef struct ctr_her_batch_t {
@@ -216,7 +222,7 @@ typedef struct ctr_her_batch_t {
     float   *next_obs;         /* [B][d]  [observation_t+1, achieved_goal_t+1, desired_goal]  */
     float   *done;             /* [B]     1 for the last real transition of an episode        */
     int32_t *index;            /* [B][3] or NULL: (slot, t, j), j = 0 real, 1..k relabelled;
-                                  slot -1: no stored row found in 256 draws                  */
+                                  slot -1: the store holds no rows (the row is zeros)        */
 } ctr_her_batch_t;
 
 /* Opens an episode for the environments with mask[i] != 0 (NULL = all) from the batch's
@@ -232,7 +238,10 @@ int ctr_her_open(const ctr_her_t *her, const ctr_batch_t *batch, const float *ob
 int ctr_her_record(const ctr_her_t *her, const ctr_batch_t *batch, const float *actions,
                    const ctr_step_out_t *out, double tol, void *stream);
 
-/* Draws B rows uniformly over the stored rows; draws are keyed (seed, counter, row). */
+/* Draws B rows uniformly with replacement over the stored rows: one uniform integer u per row
+ * (keyed seed, counter, row) below the stored-row count, mapped to its (slot, row) through the
+ * per-slot prefix sums this call rebuilds in her->cdf (exact inverse CDF: no retries, no
+ * misses whatever the episode lengths). */
 int ctr_her_sample(const ctr_her_t *her, int64_t batch_size, uint64_t seed, uint64_t counter,
                    const ctr_her_batch_t *out, void *stream);
 

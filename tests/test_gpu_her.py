@@ -118,3 +118,25 @@ def test_empty_store_returns_flagged_rows(cuda):
     env.reset()
     b = her.sample(16, return_index=True)
     assert (b["index"][:, 0] == -1).all() and len(her) == 0
+
+
+def test_one_step_episodes_never_miss(cuda):
+    """Every episode ends at its first step (tolerance 1 m): one stored row per episode against the
+    746 rows a 150-step episode holds.  The inverse-CDF draw still returns a stored row for every
+    sample (a rejection sampler over (slot, row) would miss almost every draw here)."""
+    import torch
+    from ctr_reach_amd import CtrReachVecEnv
+    gtp = dict(GTP, initial_tol=1.0, final_tol=1.0)
+    env = CtrReachVecEnv(64, device=cuda, seed=2, goal_tolerance_parameters=gtp)
+    her = env.enable_her(slots=4)
+    env.reset()
+    for _ in range(3):
+        env.step(torch.zeros((64, 6), device=cuda))
+    lens = her.len.cpu().numpy()
+    assert (lens > 0).sum() == 3 * 64 and (lens[lens > 0] == 1).all() and len(her) == 3 * 64
+    idx = her.sample(65536, return_index=True)["index"].cpu().numpy()
+    assert (idx[:, 0] >= 0).all() and (idx[:, 1] == 0).all() and (idx[:, 2] == 0).all()
+    cnt = np.bincount(idx[:, 0], minlength=len(lens))
+    assert (cnt[lens <= 0] == 0).all()
+    exp = 65536 / (3 * 64)
+    assert (np.abs(cnt[lens > 0] - exp) <= 5 * np.sqrt(exp)).all()
