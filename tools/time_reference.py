@@ -8,6 +8,7 @@ import json
 import multiprocessing as mp
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -46,6 +47,17 @@ def measure(procs, seconds):
     return sum(s for s, _ in res) / max(t for _, t in res)
 
 
+def time_port(threads, seconds):
+    """The C restatement (oracle/, bench.py's cpu_baseline leg) on this same CPU, so the GPU box's
+    cpu_baseline (kind "port") can be read against the reference: env-steps/s."""
+    code = ("import sys, json, types; sys.path.insert(0, %r); import bench; "
+            "a = types.SimpleNamespace(seed=0, cpu_seconds=%r); "
+            "print(json.dumps(bench.cpu_baseline(a, bench.CONFIGS[3])))" % (ROOT, seconds))
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = subprocess.check_output([sys.executable, "-c", code], env=env, text=True)
+    return json.loads(out.strip().splitlines()[-1])["value"]
+
+
 if __name__ == "__main__":
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     sec = float(sys.argv[2]) if len(sys.argv) > 2 else 20.0
@@ -53,7 +65,10 @@ if __name__ == "__main__":
     out = {"what": "reference CtrReachEnv.step() (scipy solve_ivp RK45), default CTR-Reach-v0 kwargs, random "
                    "actions, resets at their natural rate (included)",
            "cpu": cpu, "nproc": os.cpu_count(), "python": platform.python_version(), "seconds": sec,
-           "env_steps_per_s_1proc": measure(1, sec), "env_steps_per_s_nproc": measure(os.cpu_count(), sec)}
+           "env_steps_per_s_1proc": measure(1, sec), "env_steps_per_s_nproc": measure(os.cpu_count(), sec),
+           "port_env_steps_per_s_1thread": time_port(1, sec),
+           "port_env_steps_per_s_nthreads": time_port(os.cpu_count(), sec)}
+    out["port_over_reference_1core"] = out["port_env_steps_per_s_1thread"] / out["env_steps_per_s_1proc"]
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "cpu_reference_%s.json" % tag), "w") as fh:
         json.dump(out, fh, indent=1)
