@@ -606,6 +606,15 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         const double a30 = A30 * h, a31 = A31 * h, a32 = A32 * h;
         const double a40 = A40 * h, a41 = A41 * h, a42 = A42 * h, a43 = A43 * h;
         const double a50 = A50 * h, a51 = A51 * h, a52 = A52 * h, a53 = A53 * h, a54 = A54 * h;
+        auto c1 = [&](double k0, double y) { return fma(k0, a10, y); };
+        auto c2 = [&](double k0, double k1, double y) { return fma(k1, a21, fma(k0, a20, y)); };
+        auto c3 = [&](double k0, double k1, double k2, double y) { return fma(k2, a32, fma(k1, a31, fma(k0, a30, y))); };
+        auto c4 = [&](double k0, double k1, double k2, double k3, double y) {
+            return fma(k3, a43, fma(k2, a42, fma(k1, a41, fma(k0, a40, y))));
+        };
+        auto c5 = [&](double k0, double k1, double k2, double k3, double k4, double y) {
+            return fma(k4, a54, fma(k3, a53, fma(k2, a52, fma(k1, a51, fma(k0, a50, y)))));
+        };
 #define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF, PROW)                            \
         {                                                                                      \
             _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
@@ -624,38 +633,36 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
                 _Pragma("unroll") for (int i = 0; i < 3; ++i)                                  \
                     _Pragma("unroll") for (int j = 0; j < 4; ++j) qr[i][j] += rc[i] * PROW[j]; \
         }
-        CTR_STAGE(K1, fma(f.uz[i], a10, yu[i]),
-                  fma(f.al[i], a10, ya[i]),
-                  fma(f.R[i], a10, yR[i]), 0.0, 0.0, P1)
-        CTR_STAGE(K2, fma(K1.uz[i], a21, fma(f.uz[i], a20, yu[i])),
-                  fma(K1.al[i], a21, fma(f.al[i], a20, ya[i])),
-                  fma(K1.R[i], a21, fma(f.R[i], a20, yR[i])), B2, E2, P2)
-        CTR_STAGE(K3, fma(K2.uz[i], a32, fma(K1.uz[i], a31, fma(f.uz[i], a30, yu[i]))),
-                  fma(K2.al[i], a32, fma(K1.al[i], a31, fma(f.al[i], a30, ya[i]))),
-                  fma(K2.R[i], a32, fma(K1.R[i], a31, fma(f.R[i], a30, yR[i]))), B3, E3, P3)
-        CTR_STAGE(K4, fma(K3.uz[i], a43, fma(K2.uz[i], a42, fma(K1.uz[i], a41, fma(f.uz[i], a40, yu[i])))),
-                  fma(K3.al[i], a43, fma(K2.al[i], a42, fma(K1.al[i], a41, fma(f.al[i], a40, ya[i])))),
-                  fma(K3.R[i], a43, fma(K2.R[i], a42, fma(K1.R[i], a41, fma(f.R[i], a40, yR[i])))), B4, E4, P4)
-        CTR_STAGE(K5, fma(K4.uz[i], a54, fma(K3.uz[i], a53, fma(K2.uz[i], a52, fma(K1.uz[i], a51, fma(f.uz[i], a50, yu[i]))))),
-                  fma(K4.al[i], a54, fma(K3.al[i], a53, fma(K2.al[i], a52, fma(K1.al[i], a51, fma(f.al[i], a50, ya[i]))))),
-                  fma(K4.R[i], a54, fma(K3.R[i], a53, fma(K2.R[i], a52, fma(K1.R[i], a51, fma(f.R[i], a50, yR[i]))))), B5, E5, P5)
+        CTR_STAGE(K1, c1(f.uz[i], yu[i]), c1(f.al[i], ya[i]), c1(f.R[i], yR[i]), 0.0, 0.0, P1)
+        CTR_STAGE(K2, c2(f.uz[i], K1.uz[i], yu[i]), c2(f.al[i], K1.al[i], ya[i]), c2(f.R[i], K1.R[i], yR[i]),
+                  B2, E2, P2)
+        CTR_STAGE(K3, c3(f.uz[i], K1.uz[i], K2.uz[i], yu[i]), c3(f.al[i], K1.al[i], K2.al[i], ya[i]),
+                  c3(f.R[i], K1.R[i], K2.R[i], yR[i]), B3, E3, P3)
+        CTR_STAGE(K4, c4(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], yu[i]), c4(f.al[i], K1.al[i], K2.al[i], K3.al[i], ya[i]),
+                  c4(f.R[i], K1.R[i], K2.R[i], K3.R[i], yR[i]), B4, E4, P4)
+        CTR_STAGE(K5, c5(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], K4.uz[i], yu[i]),
+                  c5(f.al[i], K1.al[i], K2.al[i], K3.al[i], K4.al[i], ya[i]),
+                  c5(f.R[i], K1.R[i], K2.R[i], K3.R[i], K4.R[i], yR[i]), B5, E5, P5)
 #undef CTR_STAGE
         CTR_STAMP(ts2);
         // y_new (rk.py rk_step) and the error sums without K6
         double nu[3], na[3], nr[3], nR[9];
         double eu[3], ea[3], eR[9];
         const double b0 = B0 * h, b2 = B2 * h, b3 = B3 * h, b4 = B4 * h, b5 = B5 * h;
+        auto cb = [&](double k0, double k2, double k3, double k4, double k5, double y) {
+            return fma(k5, b5, fma(k4, b4, fma(k3, b3, fma(k2, b2, fma(k0, b0, y)))));
+        };
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            nu[i] = fma(K5.uz[i], b5, fma(K4.uz[i], b4, fma(K3.uz[i], b3, fma(K2.uz[i], b2, fma(f.uz[i], b0, yu[i])))));
-            na[i] = fma(K5.al[i], b5, fma(K4.al[i], b4, fma(K3.al[i], b3, fma(K2.al[i], b2, fma(f.al[i], b0, ya[i])))));
+            nu[i] = cb(f.uz[i], K2.uz[i], K3.uz[i], K4.uz[i], K5.uz[i], yu[i]);
+            na[i] = cb(f.al[i], K2.al[i], K3.al[i], K4.al[i], K5.al[i], ya[i]);
             nr[i] = yr[i] + h * br[i];
             eu[i] = f.uz[i] * E0 + K2.uz[i] * E2 + K3.uz[i] * E3 + K4.uz[i] * E4 + K5.uz[i] * E5;
             ea[i] = f.al[i] * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5;
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            nR[i] = fma(K5.R[i], b5, fma(K4.R[i], b4, fma(K3.R[i], b3, fma(K2.R[i], b2, fma(f.R[i], b0, yR[i])))));
+            nR[i] = cb(f.R[i], K2.R[i], K3.R[i], K4.R[i], K5.R[i], yR[i]);
             eR[i] = f.R[i] * E0 + K2.R[i] * E2 + K3.R[i] * E3 + K4.R[i] * E4 + K5.R[i] * E5;
         }
         Stage K6;
