@@ -934,6 +934,81 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 }
 
+// Rigid model + fixed-step RK4 with one env on a group of SEG_GROUP consecutive lanes (k_step for
+// BASELINE configs[1]): every lane segments the same joints; lane j takes the env's j-th kept
+// segment and raises its one-step map to the segment's step count (as fk_lane_rk4 does segment
+// after segment), and the group forms the ordered product M_0 M_1 ... in log2 SEG_GROUP shuffle
+// rounds.  Joints with beta <= 0 (the action Box) keep at most 6 segments: the four points
+// 0, beta_0..2 are <= 0, so the first three gaps never end after s = 0.  Every lane of the wave
+// must call it.  Tips agree with fk_lane_rk4 to rounding (the products associate differently).
+constexpr int SEG_GROUP = 8;
+
+template <bool HAS_UY, bool CAREFUL>
+__device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double tip[3], FkStats &st,
+                                double steps_per_m)
+{
+    const double beta[3] = {q[0], q[1], q[2]};
+    __shared__ double s_endg[9][CTR_BLOCK];
+    double *end_lds = &s_endg[0][threadIdx.x];
+    const Seg sg = seg_build(sy, beta, end_lds);
+    const double ya[3] = {q[3], q[4], q[5]};
+    const double yu[3] = {0.0, 0.0, 0.0};
+    const Trig tconst = trig_of<CAREFUL>(ya);
+    // the lane's kept gap (the j-th set bit) and the end of the kept gap before it
+    uint32_t rem = sg.kept;
+    double prev_end = 0.0;
+    for (int i = 0; i < j && rem != 0u; ++i) {
+        prev_end = end_lds[__builtin_ctz(rem) * CTR_BLOCK];
+        rem &= rem - 1u;
+    }
+    double aq[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, am[3] = {0.0, 0.0, 0.0};
+    int nsteps = 0;
+    if (rem != 0u) {
+        const int k = __builtin_ctz(rem);
+        const SegPar p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), true);
+        const double endk = end_lds[k * CTR_BLOCK];
+        const double a = prev_end, b = endk - 1e-6;
+        const double len = fmax(a, b) - fmin(a, b);
+        const int left = (len > 0.0) ? max(1, (int)ceil(len * steps_per_m)) : 0;
+        if (left > 0) {
+            double rq[9], rm[3];
+            rigid_step_map<HAS_UY>(p, tconst, yu, len / left, rq, rm);
+            int e = left;
+            for (;;) {
+                if (e & 1) affine_compose(aq, am, rq, rm);
+                e >>= 1;
+                if (!e) break;
+                affine_square(rq, rm);
+            }
+            nsteps = left;
+        }
+    }
+    // ordered product onto the group's lane 0: round r joins lane j with lane j + 2^r
+    #pragma unroll
+    for (int off = 1; off < SEG_GROUP; off <<= 1) {
+        double oq[9], om[3];
+        #pragma unroll
+        for (int i = 0; i < 9; ++i) oq[i] = __shfl_down(aq[i], off, SEG_GROUP);
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) om[i] = __shfl_down(am[i], off, SEG_GROUP);
+        const int on = __shfl_down(nsteps, off, SEG_GROUP);
+        if ((j & (2 * off - 1)) == 0) {
+            affine_compose(aq, am, oq, om);
+            nsteps += on;
+        }
+    }
+    // Y = [Rz(alpha_0) | 0] times the product: r = Rz(alpha_0) m  (model.py:57-60)
+    double s0, c0;
+    ctr_math::sincos_cw(ya[0], &s0, &c0);
+    tip[0] = fma(-s0, am[1], c0 * am[0]);
+    tip[1] = fma(c0, am[1], s0 * am[0]);
+    tip[2] = am[2];
+    st.nfev += 4u * (uint32_t)nsteps;
+    st.nstep += (uint32_t)nsteps;
+    st.nseg += (uint32_t)__builtin_popcount(sg.kept);
+    if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+}
+
 // ------------------------------------------------------------------------------------------
 // Env logic
 // ------------------------------------------------------------------------------------------

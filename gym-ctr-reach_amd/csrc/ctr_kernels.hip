@@ -299,19 +299,122 @@ __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict
 }
 
 // ------------------------------------------------------------------------------------------
+// The per-env tail of CtrReachEnv.step after the FK (ctr_reach_env.py:136-158): reward, done,
+// success, error, observation, and the auto-reset from the pool (or the miss flag).
+struct StepFlags {
+    bool miss = false;       // done, but no pooled reset available -> k_reset
+    bool pooled = false;     // done and reset from the pool -> queue the refill
+    uint32_t pooled_r = 0;
+};
+
+__device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o, int64_t e,
+                                            int s, float q[6], double ag[3], const FkStats &st, int32_t autoreset,
+                                            StepFlags &fl)
+{
+    const int32_t t = b.t[e] + 1;
+    double dg[3];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) dg[i] = b.desired_goal[3 * e + i];
+    const double dx = ag[0] - dg[0], dy = ag[1] - dg[1], dz = ag[2] - dg[2];
+    const double d = sqrt(dx * dx + dy * dy + dz * dz);
+    const double tol = kc.c.tol;
+    const float reward = (d > tol) ? -1.0f : 0.0f;              // ctr_reach_env.py:170
+    const bool done = (reward == 0.0f) || (t >= kc.c.max_steps); // :140
+    const bool multi = kc.c.n_systems > 1;
+    const int od = multi ? 14 : 13;
+    float obs[14];
+    obs_lane(q, dg, ag, tol, s, multi, kc.c.egocentric != 0, obs);
+    o.reward[e] = reward;
+    o.done[e] = done ? 1 : 0;
+    o.success[e] = (d < tol) ? 1 : 0;                           // :155
+    o.error[e] = (float)d;
+    uint32_t stat = st.status;
+    if (o.nfev) o.nfev[e] = st.nfev;
+    int32_t t_out = t;
+    if (autoreset && done) {
+        if (o.terminal_obs) write_obs(o.terminal_obs + od * e, obs, multi);
+        if (o.terminal_achieved)
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
+        const uint32_t r = b.epoch[e] + 1;                      // reset number to take
+        const int P = b.pool_depth;
+        const int64_t ps = P > 0 ? (int64_t)(r % (uint32_t)P) * b.n + e : 0;
+        if (P > 0 && b.pool_r[ps] == r) {
+            // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
+            const int s2 = clamp_sys(b.pool_sys[ps], kc.c.n_systems);
+            #pragma unroll
+            for (int i = 0; i < 6; ++i) q[i] = b.pool_q0[6 * ps + i];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) { dg[i] = b.pool_dg[3 * ps + i]; ag[i] = b.pool_ag[3 * ps + i]; }
+            if (b.desired_joints)
+                #pragma unroll
+                for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = b.pool_qd[6 * ps + i];
+            if (b.starting_joints)
+                #pragma unroll
+                for (int i = 0; i < 6; ++i) b.starting_joints[6 * e + i] = q[i];
+            if (b.starting_position)
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) b.starting_position[3 * e + i] = ag[i];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) b.desired_goal[3 * e + i] = dg[i];
+            b.system[e] = s2;
+            b.epoch[e] = r;
+            stat |= b.pool_stat[ps];
+            obs_lane(q, dg, ag, kc.c.tol, s2, multi, kc.c.egocentric != 0, obs);
+            fl.pooled = true;
+            fl.pooled_r = r;
+            t_out = 0;
+        } else {
+            fl.miss = true;
+        }
+    }
+    b.t[e] = t_out;
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = q[i];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) b.achieved_goal[3 * e + i] = ag[i];
+    write_obs(o.obs + od * e, obs, multi);
+    if (o.status) o.status[e] = stat;
+}
+
+// Torsionally rigid model with fixed-step RK4 (MODE bits 2 and 4): one env on a group of
+// SEG_GROUP lanes, whose segments run in parallel (fk_group_rigid4); other modes: one env per lane.
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
                                                    ctr_step_out_t o, int32_t autoreset)
 {
+    constexpr bool GROUP = (MODE & 6) == 6;
+    constexpr int G = GROUP ? SEG_GROUP : 1;
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     stage_systems(kc, s_sys, s_raw);
-    const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const bool live = e < b.n;
-    bool miss = false;       // done, but no pooled reset available -> k_reset
-    bool pooled = false;     // done and reset from the pool -> queue the refill
-    uint32_t pooled_r = 0;
-    if (live) {
+    const int64_t gl = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const int64_t e = gl / G;
+    const int j = (int)(gl % G);
+    const bool in = e < b.n;                 // the lane works on a live env
+    const bool live = in && j == 0;          // ... and is its lead lane (every per-env write)
+    StepFlags fl;
+    if constexpr (GROUP) {
+        // every lane of the wave takes part in the group's shuffles
+        int s = 0;
+        float q[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (in) {
+            s = clamp_sys(b.system[e], kc.c.n_systems);
+            float a[6];
+            #pragma unroll
+            for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
+            for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(s_sys[s], kc.c.constrain_alpha != 0, q, a);
+        }
+        const SysK &sy = in ? episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)) : s_sys[0];
+        const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
+        FkStats st = {0, 0, 0, 0, 0};
+        double ag[3];
+        if (fk_needs_careful_trig(qd))
+            fk_group_rigid4<(MODE & 1) != 0, true>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
+        else
+            fk_group_rigid4<(MODE & 1) != 0, false>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
+        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl);
+    } else if (live) {
         const int s = clamp_sys(b.system[e], kc.c.n_systems);
         const SysK &sy = s_sys[s];
         float q[6], a[6];
@@ -325,77 +428,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const fl
 #else
         fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);
 #endif
-        const int32_t t = b.t[e] + 1;
-        double dg[3];
-        #pragma unroll
-        for (int i = 0; i < 3; ++i) dg[i] = b.desired_goal[3 * e + i];
-        const double dx = ag[0] - dg[0], dy = ag[1] - dg[1], dz = ag[2] - dg[2];
-        const double d = sqrt(dx * dx + dy * dy + dz * dz);
-        const double tol = kc.c.tol;
-        const float reward = (d > tol) ? -1.0f : 0.0f;              // ctr_reach_env.py:170
-        const bool done = (reward == 0.0f) || (t >= kc.c.max_steps); // :140
-        const bool multi = kc.c.n_systems > 1;
-        const int od = multi ? 14 : 13;
-        float obs[14];
-        obs_lane(q, dg, ag, tol, s, multi, kc.c.egocentric != 0, obs);
-        o.reward[e] = reward;
-        o.done[e] = done ? 1 : 0;
-        o.success[e] = (d < tol) ? 1 : 0;                           // :155
-        o.error[e] = (float)d;
-        uint32_t stat = st.status;
-        if (o.nfev) o.nfev[e] = st.nfev;
-        int32_t t_out = t;
-        if (autoreset && done) {
-            if (o.terminal_obs) write_obs(o.terminal_obs + od * e, obs, multi);
-            if (o.terminal_achieved)
-                #pragma unroll
-                for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
-            const uint32_t r = b.epoch[e] + 1;                      // reset number to take
-            const int P = b.pool_depth;
-            const int64_t ps = P > 0 ? (int64_t)(r % (uint32_t)P) * b.n + e : 0;
-            if (P > 0 && b.pool_r[ps] == r) {
-                // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
-                const int s2 = clamp_sys(b.pool_sys[ps], kc.c.n_systems);
-                #pragma unroll
-                for (int i = 0; i < 6; ++i) q[i] = b.pool_q0[6 * ps + i];
-                #pragma unroll
-                for (int i = 0; i < 3; ++i) { dg[i] = b.pool_dg[3 * ps + i]; ag[i] = b.pool_ag[3 * ps + i]; }
-                if (b.desired_joints)
-                    #pragma unroll
-                    for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = b.pool_qd[6 * ps + i];
-                if (b.starting_joints)
-                    #pragma unroll
-                    for (int i = 0; i < 6; ++i) b.starting_joints[6 * e + i] = q[i];
-                if (b.starting_position)
-                    #pragma unroll
-                    for (int i = 0; i < 3; ++i) b.starting_position[3 * e + i] = ag[i];
-                #pragma unroll
-                for (int i = 0; i < 3; ++i) b.desired_goal[3 * e + i] = dg[i];
-                b.system[e] = s2;
-                b.epoch[e] = r;
-                stat |= b.pool_stat[ps];
-                obs_lane(q, dg, ag, kc.c.tol, s2, multi, kc.c.egocentric != 0, obs);
-                pooled = true;
-                pooled_r = r;
-                t_out = 0;
-            } else {
-                miss = true;
-            }
-        }
-        b.t[e] = t_out;
-        #pragma unroll
-        for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = q[i];
-        #pragma unroll
-        for (int i = 0; i < 3; ++i) b.achieved_goal[3 * e + i] = ag[i];
-        write_obs(o.obs + od * e, obs, multi);
-        if (o.status) o.status[e] = stat;
+        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl);
     }
     if (autoreset) {
         const int32_t one[1] = {(int32_t)e};
-        wave_append(miss_counter(b), miss_items(b), b.n, miss, one, 1);
+        wave_append(miss_counter(b), miss_items(b), b.n, fl.miss, one, 1);
         if (b.pool_depth > 0) {
-            const int32_t two[2] = {(int32_t)e, (int32_t)(pooled_r + (uint32_t)b.pool_depth)};
-            wave_append(b.refill, b.refill + 1, b.refill_cap, pooled, two, 2);
+            const int32_t two[2] = {(int32_t)e, (int32_t)(fl.pooled_r + (uint32_t)b.pool_depth)};
+            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
         }
     }
 }
@@ -769,7 +809,8 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(b.n)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+    const int64_t lanes = (kc.mode & 6) == 6 ? SEG_GROUP * b.n : b.n;      // k_step's lanes per env
+    CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset) {
         // misses are rare with a pool: a small grid sweeps the list grid-stride

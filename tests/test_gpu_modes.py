@@ -51,6 +51,7 @@ def test_step_modes_vs_oracle(cuda, oracle_mod, integrator, spm, model):
     n = 4096
     env = CtrReachVecEnv(n, device=cuda, seed=5, select_systems=[0, 1, 2, 3], autoreset=False,
                          integrator=integrator, rk4_steps_per_m=spm, model=model)
+    env.enable_nfev()
     env.reset()
     rng = np.random.default_rng(3)
     hi = env.action_space.high
@@ -69,6 +70,8 @@ def test_step_modes_vs_oracle(cuda, oracle_mod, integrator, spm, model):
         np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"].astype(np.float32))
         np.testing.assert_array_equal(done.cpu().numpy(), ref["done"])
         assert np.abs(obs["observation"].cpu().numpy() - ref["observation"]).max() < 1e-6
+        # RHS counts (rigid RK4: the lane group's summed 4 n per segment)
+        assert (env.nfev.cpu().numpy() == ref["nfev"]).mean() > 0.999
         if done.any():
             break
 
