@@ -41,15 +41,19 @@ def unpack_step_outputs(packed):
     return packed[:, 0:3], packed[:, 3], (flags & 1).bool(), (flags & 2).bool()
 
 
-def all_gather_outputs(packed, group=None):
+def all_gather_outputs(packed, group=None, async_op=False):
     """All-gather every rank's packed [n, 5] block into [world * n, 5] (rank-major = global id
-    order).  Uses all_gather_into_tensor: one RCCL ring/tree call for the whole step."""
+    order).  Uses all_gather_into_tensor: one RCCL ring/tree call for the whole step.
+
+    async_op=True returns (out, work): the collective runs on RCCL's own stream, ordered after
+    the packing on the current stream, so the next ctr_step overlaps it; ``work.wait()`` before
+    reading ``out``, and keep ``packed`` unchanged until then."""
     import torch
     import torch.distributed as dist
     ws = dist.get_world_size(group)
     out = torch.empty((ws * packed.shape[0], packed.shape[1]), dtype=packed.dtype, device=packed.device)
-    dist.all_gather_into_tensor(out, packed.contiguous(), group=group)
-    return out
+    work = dist.all_gather_into_tensor(out, packed.contiguous(), group=group, async_op=async_op)
+    return (out, work) if async_op else out
 
 
 def max_over_ranks(value, device=None, group=None):

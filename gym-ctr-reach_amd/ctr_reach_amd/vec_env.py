@@ -380,16 +380,21 @@ class CtrReachVecEnv(object):
         out["table"] = table
         return out
 
-    def gather_outputs(self, group=None):
+    def gather_outputs(self, group=None, async_op=False):
         """Optional collective for a single-process trainer: every rank's last-step (tip, reward,
         done, success) packed to 20 B/env and all-gathered over RCCL -> [world * n, 5] float32
-        in global-id order.  Not used on the stepping path."""
+        in global-id order.  Not used on the stepping path.  async_op=True returns (out, work)
+        and lets the next step() run while the gather is in flight (RCCL's stream); the pack
+        buffers alternate, so one gather may be outstanding per env."""
         import torch
         from . import distributed as D
         d = self.done.bool()
         tip = torch.where(d[:, None], self.terminal_achieved, self.achieved_goal) if self.autoreset else self.achieved_goal
-        self._packed = D.pack_step_outputs(tip, self.reward, d, self.success, out=getattr(self, "_packed", None))
-        return D.all_gather_outputs(self._packed, group=group)
+        bufs = getattr(self, "_packed", None) or [None, None]
+        k = getattr(self, "_packed_k", 0)
+        bufs[k] = D.pack_step_outputs(tip, self.reward, d, self.success, out=bufs[k])
+        self._packed, self._packed_k = bufs, k ^ 1
+        return D.all_gather_outputs(bufs[k], group=group, async_op=async_op)
 
     def update_goal_tolerance(self, timestep):
         self.goal_tolerance.update(timestep)

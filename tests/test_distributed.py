@@ -41,6 +41,9 @@ def _worker(rank, world, port, n, q):
         packed = D.pack_step_outputs(torch.tensor(r["achieved_goal"]), torch.tensor(r["reward"], dtype=torch.float32),
                                      torch.tensor(r["done"]), torch.tensor(r["is_success"]))
         full = D.all_gather_outputs(packed)
+        full_async, work = D.all_gather_outputs(packed, async_op=True)     # overlapped form
+        work.wait()
+        assert torch.equal(full, full_async)
         t = D.max_over_ranks(0.5 + rank)
         if rank == 0:
             q.put((full.numpy(), t))

@@ -1,0 +1,52 @@
+"""The optional RCCL all-gather of packed step outputs (CtrReachVecEnv.gather_outputs) on the GPU,
+in a one-rank process group (the multi-rank logic is covered with gloo in test_distributed.py):
+synchronous and overlapped (async_op) forms, and a step launched while the gather is in flight.
+
+Bars: the gathered block equals the env's own (tip as float32, reward, done | success << 1)
+bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gather_outputs_over_rccl(cuda):
+    import torch
+    import torch.distributed as dist
+    from ctr_reach_amd import CtrReachVecEnv
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    try:
+        n = 1024
+        env = CtrReachVecEnv(n, device=cuda, seed=4)
+        env.reset()
+        g = torch.Generator(device=cuda)
+        g.manual_seed(2)
+        hi = torch.tensor(env.action_space.high, device=cuda)
+        act = lambda: ((torch.rand((n, 6), generator=g, device=cuda) * 2 - 1) * hi).contiguous()  # noqa: E731
+        env.step(act())
+        full = env.gather_outputs()
+        d = env.done.bool()
+        tip = torch.where(d[:, None], env.terminal_achieved, env.achieved_goal).float()
+        want = torch.cat([tip, env.reward[:, None], (env.done.float() + 2 * env.success.float())[:, None]], 1)
+        assert torch.equal(full, want)
+        # overlapped: the gather of step k runs while step k + 1 is launched
+        out, work = env.gather_outputs(async_op=True)
+        want = want.clone()
+        env.step(act())
+        work.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want)
+    finally:
+        dist.destroy_process_group()
