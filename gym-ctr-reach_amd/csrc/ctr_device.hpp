@@ -22,6 +22,7 @@ namespace ctr {
 
 constexpr int NS = 18;  // [u_z(3), alpha(3), r(3), R row-major(9)]   (model.py:136)
 constexpr int CTR_BLOCK = 256;   // every kernel runs 256-lane workgroups (per-lane LDS slots below)
+constexpr int RK4_MAX_STEPS = 1 << 20;   // fixed-step RK4: more steps in one segment -> CTR_STATUS_TOO_LONG
 
 // ------------------------------------------------------------------------------------------
 // Segmentation (Segment.py:6-61).  Ten transition points [0, beta, d_c, d_tip] are sorted,
@@ -576,8 +577,13 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             rejected = new_step ? false : rejected;
             new_step = false;
         }
-        if (ha < min_step) {                         // TOO_SMALL_STEP -> solver failed
-            st.status |= CTR_STATUS_STEP_UNDERFLOW;
+        if (!(ha >= min_step)) {                     // TOO_SMALL_STEP -> solver failed
+            if (ha < min_step) {
+                st.status |= CTR_STATUS_STEP_UNDERFLOW;
+            } else {                                 // NaN step size (NaN joints): scipy would
+                yr[0] = yr[1] = yr[2] = NAN;         // loop forever (as in the gap case)
+                st.status |= CTR_STATUS_NAN;
+            }
             break;
         }
         double tnew = t + ha;
@@ -861,7 +867,13 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
             const double len = fmax(a, b) - fmin(a, b);
             prev_end = endk;
             st.nseg++;
-            left = (len > 0.0) ? max(1, (int)ceil(len * steps_per_m)) : 0;
+            const double nf = ceil(len * steps_per_m);
+            if (len > 0.0 && !(nf <= (double)RK4_MAX_STEPS)) {   // joints far outside the Box
+                yr[0] = yr[1] = yr[2] = NAN;
+                st.status |= CTR_STATUS_TOO_LONG | CTR_STATUS_NAN;
+                break;
+            }
+            left = (len > 0.0) ? max(1, (int)nf) : 0;
             h = (left > 0) ? len / left : 0.0;
             if (RIGID) {
                 rigid_step_map<HAS_UY>(p, tconst, yu, h, rq, rm);
@@ -963,13 +975,16 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     }
     double aq[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, am[3] = {0.0, 0.0, 0.0};
     int nsteps = 0;
+    bool too_long = false;
     if (rem != 0u) {
         const int k = __builtin_ctz(rem);
         const SegPar p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), true);
         const double endk = end_lds[k * CTR_BLOCK];
         const double a = prev_end, b = endk - 1e-6;
         const double len = fmax(a, b) - fmin(a, b);
-        const int left = (len > 0.0) ? max(1, (int)ceil(len * steps_per_m)) : 0;
+        const double nf = ceil(len * steps_per_m);
+        too_long = len > 0.0 && !(nf <= (double)RK4_MAX_STEPS);
+        const int left = (len > 0.0 && !too_long) ? max(1, (int)nf) : 0;
         if (left > 0) {
             double rq[9], rm[3];
             rigid_step_map<HAS_UY>(p, tconst, yu, len / left, rq, rm);
@@ -983,6 +998,10 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
             nsteps = left;
         }
     }
+    if (too_long) am[0] = NAN;                       // the product (and the tip) turns NaN
+    int any_long = too_long ? 1 : 0;
+    #pragma unroll
+    for (int off = 1; off < SEG_GROUP; off <<= 1) any_long |= __shfl_xor(any_long, off, SEG_GROUP);
     // ordered product onto the group's lane 0: round r joins lane j with lane j + 2^r
     #pragma unroll
     for (int off = 1; off < SEG_GROUP; off <<= 1) {
@@ -1006,6 +1025,7 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     st.nfev += 4u * (uint32_t)nsteps;
     st.nstep += (uint32_t)nsteps;
     st.nseg += (uint32_t)__builtin_popcount(sg.kept);
+    if (any_long) st.status |= CTR_STATUS_TOO_LONG;
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 }
 

@@ -20,6 +20,7 @@ CTR_MODEL_RIGID = 1
 CTR_STATUS_STEP_UNDERFLOW = 1
 CTR_STATUS_SAMPLER_STUCK = 2
 CTR_STATUS_NAN = 4
+CTR_STATUS_TOO_LONG = 8
 CTR_HER_FUTURE = 0
 CTR_HER_FINAL = 1
 CTR_HER_EPISODE = 2

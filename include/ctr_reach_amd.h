@@ -55,6 +55,8 @@ extern "C" {
 #define CTR_STATUS_STEP_UNDERFLOW 1u   /* scipy "Required step size is less than spacing" */
 #define CTR_STATUS_SAMPLER_STUCK  2u   /* obs.py:204 "Stuck sampling goals..." (>1000 tries) */
 #define CTR_STATUS_NAN            4u   /* model.py:69 assert not any(isnan(r)) */
+#define CTR_STATUS_TOO_LONG       8u   /* fixed-step RK4: a segment needs > 2^20 steps (joints far
+                                           outside the action box); the tip is NaN          */
 
 /* One 3-tube system (index 0 = innermost tube), derived on the host from the
  * registration kwargs exactly as Tube.__init__ (envs/CTR_Python/Tube.py:7-19):

@@ -124,3 +124,31 @@ def test_fk_huge_angles_vs_oracle(cuda, oracle_mod):
     assert err[big].max() < 1e-6, err[big].max()
     assert err[~big].max() < 1e-10, err[~big].max()
     assert np.isfinite(tip.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("integrator,spm,model", [("rk45_scipy", 100, "compliant"), ("rk4", 100, "compliant"),
+                                                  ("rk4", 100, "rigid")])
+def test_nan_and_far_joints_terminate(cuda, integrator, spm, model):
+    """FK inputs the reference cannot integrate end with a status flag instead of a hang: NaN
+    angles (scipy would loop on a NaN step size) -> NAN / STEP_UNDERFLOW; a fixed-step RK4
+    segment of more than 2^20 steps -> TOO_LONG with a NaN tip.  The env's own step (the 8-lane
+    group path for the rigid model) is bounded the same way."""
+    import torch
+    from ctr_reach_amd import CtrReachVecEnv, _abi
+    q = np.array([[-0.1, -0.05, -0.02, np.nan, 0.2, 0.3],
+                  [-0.1, -0.05, -0.02, 0.1, np.nan, 0.3],
+                  [np.nan, -0.05, -0.02, 0.1, 0.2, 0.3],
+                  [5e4, -0.05, -0.02, 0.1, 0.2, 0.3]], np.float32)
+    env = CtrReachVecEnv(4, device=cuda, seed=1, integrator=integrator, rk4_steps_per_m=spm, model=model)
+    tip, st = env.forward_kinematics(torch.tensor(q, device=cuda), return_stats=True)
+    torch.cuda.synchronize()
+    status = st["status"].cpu().numpy()
+    assert (status[:2] & (_abi.CTR_STATUS_NAN | _abi.CTR_STATUS_STEP_UNDERFLOW)).all()
+    if integrator == "rk4":
+        assert status[3] & _abi.CTR_STATUS_TOO_LONG and np.isnan(tip.cpu().numpy()[3]).all()
+    else:
+        assert status[3] & _abi.CTR_STATUS_NAN                      # the tube gap [0, 5e4]
+    env.reset()
+    env.joints.copy_(torch.tensor(q, device=cuda))
+    env.step(torch.zeros((4, 6), device=cuda))
+    torch.cuda.synchronize()

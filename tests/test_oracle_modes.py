@@ -112,3 +112,20 @@ def test_backbone_shape_vs_reference(golden_dir, oracle_mod):
         L = [sy[s].L[k] for k in range(3)]
         ti = oracle_mod.tube_tip_indices(o["s"][i, :o["npts"][i]], L, d["joints"][i, :3].astype(np.float64))
         np.testing.assert_array_equal(ti, d["tip_idx"][i])
+
+
+@pytest.mark.timeout(120)
+def test_oracle_terminates_on_nan_and_far_joints():
+    """Inputs the reference cannot integrate (scipy loops forever on a NaN step size, as in the
+    tube-gap case) end with a flag: NaN angles -> CTR_STATUS_NAN / STEP_UNDERFLOW; a fixed-step
+    RK4 segment needing more than 2^20 steps -> CTR_STATUS_TOO_LONG with a NaN tip."""
+    import oracle
+    q = np.array([[np.nan, -0.05, -0.02, 0.1, 0.2, 0.3],
+                  [-0.1, -0.05, -0.02, np.nan, 0.2, 0.3],
+                  [-0.1, -0.05, -0.02, 0.1, np.nan, 0.3],
+                  [5e4, -0.05, -0.02, 0.1, 0.2, 0.3]], np.float32)
+    r = oracle.fk(q)
+    assert (r["status"][1:] & 5).all() and np.isnan(r["tip"][1:]).all()
+    for model in ("compliant", "rigid"):
+        r = oracle.fk(q, integrator="rk4", steps_per_m=100, model=model)
+        assert r["status"][3] & 8 and np.isnan(r["tip"][3]).all()
