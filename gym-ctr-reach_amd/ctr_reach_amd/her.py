@@ -84,12 +84,12 @@ class HerReplayBuffer(object):
     # called by CtrReachVecEnv
     def _open(self, mask, stream):
         rc = self.lib.ctr_her_open(self._h, self.venv._batch, _abi.ptr(self.venv.obs), _abi.ptr(mask),
-                                   _abi.stream_ptr(stream))
+                                   _abi.stream_ptr(stream, self.venv.device.index))
         _abi.check(rc, "ctr_her_open")
 
     def _record(self, actions, stream):
         rc = self.lib.ctr_her_record(self._h, self.venv._batch, _abi.ptr(actions), self.venv._out,
-                                     float(self.venv.cfg.tol), _abi.stream_ptr(stream))
+                                     float(self.venv.cfg.tol), _abi.stream_ptr(stream, self.venv.device.index))
         _abi.check(rc, "ctr_her_record")
 
     def rows_per_episode(self, L):
@@ -122,7 +122,7 @@ class HerReplayBuffer(object):
                                                                         p(out["reward"]), p(out["next_obs"]),
                                                                         p(out["done"]), p(idx))
         s = (self.seed ^ 0x5DEECE66D) if seed is None else int(seed)
-        rc = self.lib.ctr_her_sample(self._h, B, s & 0xFFFFFFFFFFFFFFFF, self._counter, hb, _abi.stream_ptr(stream))
+        rc = self.lib.ctr_her_sample(self._h, B, s & 0xFFFFFFFFFFFFFFFF, self._counter, hb, _abi.stream_ptr(stream, self.venv.device.index))
         _abi.check(rc, "ctr_her_sample")
         self._counter += 1
         if return_index:

@@ -271,8 +271,8 @@ class CtrReachVecEnv(object):
 
     def step_raw(self, actions, stream=None):
         """step() without building Python return values (benchmark / graph capture)."""
-        rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
-                               _abi.stream_ptr(stream))
+        sp = _abi.stream_ptr(stream, self.device.index)
+        rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset), sp)
         if rc:
             _abi.check(rc, "ctr_step")
         if self._her is not None:
