@@ -5,7 +5,8 @@
 //   k_set_action  n_substeps x Obs.set_action                          (envs/obs.py:166-183)
 //   k_step        fused CtrReachEnv.step: set_action x n_substeps, FK, reward, done,
 //                 success, error, observation; a done env takes its next reset from the
-//                 reset pool (a copy), or is queued for k_reset      (envs/ctr_reach_env.py:124-158)
+//                 reset pool (a copy), or is queued for k_reset      (envs/ctr_reach_env.py:124-158);
+//                 rigid model + fixed-step RK4: one env per 8-lane group (fk_group_rigid4)
 //   k_reset       CtrReachEnv.reset, TWO lanes per env (goal FK | start FK in parallel),
 //                 for the queued / masked envs                        (envs/ctr_reach_env.py:70-114)
 //   k_refill      precomputes queued resets into the pool, two lanes per reset
@@ -13,7 +14,8 @@
 //   k_fk_shape    FK + backbone shape r at 30 dense-output points/segment (envs/model.py:66-68,119-174)
 //   k_jacobian    forward-difference tip Jacobian, 7 lanes per env       (CTR_Python/CTR_Model.py:251-262)
 //   k_domain_params  each env's current (domain-randomised) tube table  (envs/model.py:20-28)
-//   k_her_*       HER replay feed: episode recording, relabelled uniform sampling (ctr_her.inc)
+//   k_her_*       HER replay feed: episode recording, row prefix sums, relabelled uniform
+//                 sampling by inverse CDF (ctr_her.inc)
 //
 // Work lists (auto-reset misses, pool refills) are appended with one wave-aggregated atomic per
 // wave.  The tube tables (<= 8 systems x 18 doubles) travel as a kernel argument and are staged
