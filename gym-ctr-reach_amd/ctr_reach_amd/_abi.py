@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 7
+CTR_ABI_VERSION = 8
 CTR_MAX_SYSTEMS = 8
 CTR_HER_SCAN_TILE = 1024
 CTR_INTEGRATOR_RK45_SCIPY = 0
@@ -131,7 +131,7 @@ class CtrHerBatch(ctypes.Structure):
 
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
             "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
-            "ctr_her_open", "ctr_her_record", "ctr_her_sample")
+            "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her")
 
 _lib = None
 
@@ -168,9 +168,11 @@ def load(path=None):
                                  ctypes.c_double, _P]
     L.ctr_her_sample.argtypes = [ctypes.POINTER(CtrHer), i64, ctypes.c_uint64, ctypes.c_uint64,
                                  ctypes.POINTER(CtrHerBatch), _P]
+    L.ctr_step_her.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P,
+                               ctypes.POINTER(CtrStepOut), i32, ctypes.POINTER(CtrHer), _P]
     for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward",
                "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
-               "ctr_her_open", "ctr_her_record", "ctr_her_sample"):
+               "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her"):
         getattr(L, fn).restype = ctypes.c_int
     if L.ctr_abi_version() != CTR_ABI_VERSION:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))

@@ -272,11 +272,13 @@ class CtrReachVecEnv(object):
     def step_raw(self, actions, stream=None):
         """step() without building Python return values (benchmark / graph capture)."""
         sp = _abi.stream_ptr(stream, self.device.index)
-        rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset), sp)
+        if self._her is None:
+            rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset), sp)
+        else:      # the step records itself into the HER store (ctr_step_her)
+            rc = self.lib.ctr_step_her(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
+                                       self._her._h, sp)
         if rc:
             _abi.check(rc, "ctr_step")
-        if self._her is not None:
-            self._her._record(actions, stream)
         if self.autoreset:
             self._batch.work_parity ^= 1
         if self.pool_depth:

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 7
+#define CTR_ABI_VERSION 8
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -239,6 +239,13 @@ int ctr_her_open(const ctr_her_t *her, const ctr_batch_t *batch, const float *ob
  * state. */
 int ctr_her_record(const ctr_her_t *her, const ctr_batch_t *batch, const float *actions,
                    const ctr_step_out_t *out, double tol, void *stream);
+
+/* ctr_step + ctr_her_record in one pass: k_step writes the step's transition into the store as
+ * it finishes each env (no second launch, no re-read of the step outputs), and opens the next
+ * episode of every env it auto-resets (the miss sweep does it for the envs it resets).  Same
+ * arguments and outputs as ctr_step; terminal_obs / terminal_achieved may be NULL here. */
+int ctr_step_her(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float *actions,
+                 const ctr_step_out_t *out, int32_t autoreset, const ctr_her_t *her, void *stream);
 
 /* Draws B rows uniformly with replacement over the stored rows: one uniform integer u per row
  * (keyed seed, counter, row) below the stored-row count, mapped to its (slot, row) through the

@@ -15,12 +15,12 @@ GTP = {"inc_tol_obs": False, "final_tol": 0.001, "initial_tol": 0.05, "N_ts": 10
        "set_tol": 0}
 
 
-def _run(cuda, n=48, steps=60, t_max=12, slots=4, strategy="future", k=4, select_systems=(0,)):
+def _run(cuda, n=48, steps=60, t_max=12, slots=4, strategy="future", k=4, select_systems=(0,), **envkw):
     import torch
     import her_oracle as H
     from ctr_reach_amd import CtrReachVecEnv
     env = CtrReachVecEnv(n, device=cuda, seed=5, max_steps_per_episode=t_max, goal_tolerance_parameters=GTP,
-                         select_systems=list(select_systems))
+                         select_systems=list(select_systems), **envkw)
     her = env.enable_her(slots=slots, n_sampled_goal=k, goal_selection_strategy=strategy)
     env.reset()
     tol = env.get_goal_tolerance()
@@ -140,3 +140,24 @@ def test_one_step_episodes_never_miss(cuda):
     assert (cnt[lens <= 0] == 0).all()
     exp = 65536 / (3 * 64)
     assert (np.abs(cnt[lens > 0] - exp) <= 5 * np.sqrt(exp)).all()
+
+
+def test_rows_match_when_resets_miss_the_pool(cuda, oracle_mod):
+    """A one-deep reset pool that is never refilled: from each env's second auto-reset on, the
+    reset misses the pool and the sweep (k_reset) resets the env and opens its next HER episode.
+    Rows stay bit-equal to the restatement's."""
+    env, her, rec = _run(cuda, n=32, steps=40, pool_depth=1, refill_interval=100000)
+    lens, eps = her.len.cpu().numpy(), her.epoch.cpu().numpy()
+    stored = np.where(lens > 0)[0]
+    assert len(stored) > 64
+    for s in stored:
+        key = (s // her.slots, int(eps[s]))
+        assert key in rec.lengths and rec.lengths[key] == lens[s]
+    b = her.sample(4096, return_index=True)
+    idx = b["index"].cpu().numpy()
+    got = {k: b[k].cpu().numpy() for k in ("obs", "next_obs", "action", "reward")}
+    for i, (s, t, j) in enumerate(idx):
+        row = rec.stored[(s // her.slots, int(eps[s]))][(t, j)]
+        np.testing.assert_array_equal(got["obs"][i], row["obs"])
+        np.testing.assert_array_equal(got["next_obs"][i], row["next_obs"])
+        assert got["reward"][i] == row["reward"]

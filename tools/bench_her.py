@@ -68,6 +68,19 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize()
     smp_ms = e0.elapsed_time(e1) / K
+    # the fused path (ctr_step_her) against the same steps without recording
+    def step_us(with_her):
+        keep = env._her
+        env._her = keep if with_her else None
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for i in range(K):
+            env.step_raw(acts[i % 8])
+        e1.record(stream)
+        torch.cuda.synchronize()
+        env._her = keep
+        return e0.elapsed_time(e1) / K * 1e3
+    plain_us, fused_us = step_us(False), step_us(True)
     d = env.obs_dim
     # algorithmic bytes: record reads action 24 + reward 4 + done 1 + t 4 + cur_t/epoch 8 + obs_{t+1}
     # 4d + ag 24 (+ terminal selects), writes action 24 + reward 4 + obs 4d + ag 24 + cur_t 4
@@ -79,7 +92,8 @@ def main():
         "envs": args.envs, "slots": args.slots, "store_bytes": her.nbytes, "stored_rows": len(her),
         "record_us": rec_ms * 1e3, "record_bytes": rec_bytes, "record_gbs": rec_bytes / (rec_ms * 1e-3) / 1e9,
         "sample_rows": args.batch, "sample_us": smp_ms * 1e3, "sample_bytes": smp_bytes,
-        "sample_gbs": smp_bytes / (smp_ms * 1e-3) / 1e9, "rows_per_s": args.batch / (smp_ms * 1e-3)}))
+        "sample_gbs": smp_bytes / (smp_ms * 1e-3) / 1e9, "rows_per_s": args.batch / (smp_ms * 1e-3),
+        "step_us": plain_us, "step_her_fused_us": fused_us}))
 
 
 if __name__ == "__main__":
