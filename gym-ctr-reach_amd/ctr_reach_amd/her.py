@@ -73,6 +73,7 @@ class HerReplayBuffer(object):
         h.dg, h.tol, h.len, h.epoch = p(self.dg), p(self.tol), p(self.len), p(self.epoch)
         h.cur_t, h.cur_epoch, h.cdf = p(self.cur_t), p(self.cur_epoch), p(self.cdf)
         self._counter = 0
+        self.fused = True        # record inside the step (ctr_step_her); False: ctr_her_record after it
         venv._her = self
 
     @property

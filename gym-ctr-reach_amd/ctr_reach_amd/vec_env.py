@@ -272,13 +272,16 @@ class CtrReachVecEnv(object):
     def step_raw(self, actions, stream=None):
         """step() without building Python return values (benchmark / graph capture)."""
         sp = _abi.stream_ptr(stream, self.device.index)
-        if self._her is None:
-            rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset), sp)
-        else:      # the step records itself into the HER store (ctr_step_her)
+        her = self._her
+        if her is not None and her.fused:      # the step records itself into the HER store (ctr_step_her)
             rc = self.lib.ctr_step_her(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
-                                       self._her._h, sp)
+                                       her._h, sp)
+        else:
+            rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset), sp)
         if rc:
             _abi.check(rc, "ctr_step")
+        if her is not None and not her.fused:  # ctr_her_record from the step's outputs
+            her._record(actions, stream)
         if self.autoreset:
             self._batch.work_parity ^= 1
         if self.pool_depth:

@@ -15,13 +15,14 @@ GTP = {"inc_tol_obs": False, "final_tol": 0.001, "initial_tol": 0.05, "N_ts": 10
        "set_tol": 0}
 
 
-def _run(cuda, n=48, steps=60, t_max=12, slots=4, strategy="future", k=4, select_systems=(0,), **envkw):
+def _run(cuda, n=48, steps=60, t_max=12, slots=4, strategy="future", k=4, select_systems=(0,), fused=True, **envkw):
     import torch
     import her_oracle as H
     from ctr_reach_amd import CtrReachVecEnv
     env = CtrReachVecEnv(n, device=cuda, seed=5, max_steps_per_episode=t_max, goal_tolerance_parameters=GTP,
                          select_systems=list(select_systems), **envkw)
     her = env.enable_her(slots=slots, n_sampled_goal=k, goal_selection_strategy=strategy)
+    her.fused = fused
     env.reset()
     tol = env.get_goal_tolerance()
     rec = H.EpisodeRecorder(n, k=k, strategy=strategy, seed=her.seed)
@@ -50,9 +51,10 @@ def _run(cuda, n=48, steps=60, t_max=12, slots=4, strategy="future", k=4, select
     return env, her, rec
 
 
-@pytest.mark.parametrize("strategy,systems", [("future", (0,)), ("final", (0, 1, 2, 3)), ("episode", (0,))])
-def test_sampled_rows_match_restatement(cuda, oracle_mod, strategy, systems):
-    env, her, rec = _run(cuda, strategy=strategy, select_systems=systems)
+@pytest.mark.parametrize("strategy,systems,fused", [("future", (0,), True), ("final", (0, 1, 2, 3), True),
+                                                    ("episode", (0,), True), ("future", (0,), False)])
+def test_sampled_rows_match_restatement(cuda, oracle_mod, strategy, systems, fused):
+    env, her, rec = _run(cuda, strategy=strategy, select_systems=systems, fused=fused)
     lens, eps = her.len.cpu().numpy(), her.epoch.cpu().numpy()
     stored = np.where(lens > 0)[0]
     assert len(stored) > 100
@@ -146,7 +148,12 @@ def test_rows_match_when_resets_miss_the_pool(cuda, oracle_mod):
     """A one-deep reset pool that is never refilled: from each env's second auto-reset on, the
     reset misses the pool and the sweep (k_reset) resets the env and opens its next HER episode.
     Rows stay bit-equal to the restatement's."""
-    env, her, rec = _run(cuda, n=32, steps=40, pool_depth=1, refill_interval=100000)
+    for fused in (True, False):
+        _check_pool_misses(cuda, fused)
+
+
+def _check_pool_misses(cuda, fused):
+    env, her, rec = _run(cuda, n=32, steps=40, pool_depth=1, refill_interval=100000, fused=fused)
     lens, eps = her.len.cpu().numpy(), her.epoch.cpu().numpy()
     stored = np.where(lens > 0)[0]
     assert len(stored) > 64
