@@ -3,13 +3,24 @@
 
 Workload (BASELINE.json configs[2], the headline): 65 536 parallel 3-tube envs per GPU,
 torsionally-compliant model, scipy-faithful RK45 (parity mode, fp64), default CTR-Reach-v0
-kwargs (system 0, n_substeps 10, tol 0.020 m, max 150 steps), synthetic uniform actions,
-auto-resets at their natural rate inside the timed region.  A "step" = one batched
-CtrReachVecEnv.step over all envs of the GPU.
+kwargs (system 0, n_substeps 10, tol 0.020 m, max 150 steps), synthetic uniform actions.
+A "step" = one batched CtrReachVecEnv.step over all envs of the GPU.
 
-Multi-GPU (``torchrun --nproc-per-node N``): one process per GPU, contiguous shards of the
-global env id space (env_base = rank * n), no collective on the data path (weak scaling);
-a barrier + device sync bracket the timed region and the time is the MAX over ranks.
+Steady state ("including auto-resets at their natural rate"): the episode
+clocks t are staggered uniformly over [0, max_steps) and the batch runs max_steps untimed
+steps first, so time-limit resets arrive every step at the rate of a long-running trainer
+(about n / 150 per step, plus successes).  The reset-pool refill interval is chosen to divide
+the timed steps (largest divisor <= 64) and the window starts right after a refill, so the
+window holds exactly steps / interval refills, each precomputing the resets the window itself
+consumed.  resets_in_window and refills_in_window are reported.
+
+Multi-GPU: ``python bench.py --gpus N`` launches N ranks itself (one process per GPU, before
+anything touches a GPU); under ``torch.distributed.run`` the ranks come from the environment.
+Rank r owns the contiguous global env ids [r n, (r + 1) n) (weak scaling, no collective on the
+step itself).  With N > 1 every timed step also all-gathers the packed step outputs (20 B/env:
+tip, reward, done | success) over RCCL -- BASELINE configs[3] -- asynchronously on RCCL's
+stream while the next step runs; k_step writes the packed rows itself (pack_outputs).  A
+barrier + device sync bracket the timed region and the time is the MAX over ranks.
 
 Also reported: the dominant kernel's roofline (algorithmic FP64 flops / its average launch
 time measured with HIP events on the launch stream) and the CPU oracle timed on this host
@@ -39,7 +50,7 @@ BYTES_STEP = 170        # algorithmic bytes per env-step
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128, help="timed steps (a multiple of the 64-step pool refill by default)")
+    ap.add_argument("--steps", type=int, default=128, help="timed steps")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 5),
                     help="BASELINE.json config (1-based): 3 = headline (65 536 envs, compliant, scipy RK45); "
@@ -50,33 +61,77 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--profile-only", action="store_true", help="no timing extras (for rocprofv3)")
-    ap.add_argument("--refill-interval", type=int, default=None, help="reset-pool refill interval (steps)")
+    ap.add_argument("--refill-interval", type=int, default=None,
+                    help="reset-pool refill interval (steps); default: the largest divisor of --steps <= 64")
+    ap.add_argument("--gather", choices=("auto", "on", "off"), default="auto",
+                    help="RCCL all-gather of the packed step outputs in every timed step (auto: on when N > 1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group check only (CPU, gloo): no GPU, no env, no bench line")
+    ap.add_argument("--no-stagger", action="store_true",
+                    help="start every episode at t = 0 (synchronised resets; not the steady state)")
     ap.add_argument("--systems", default="0",
                     help="select_systems, comma-separated registration indices (default 0, the headline; "
                          "'0,1,2,3' is SURVEY.md 8(d)'s mixed-system divergence check)")
     return ap.parse_args()
 
 
-def dist_init():
-    """One process per GPU (torchrun).  RCCL (backend "nccl") by default.  Rehearsal overrides for
-    a one-GPU box: CTR_BENCH_BACKEND=gloo with CTR_BENCH_SAME_DEVICE=1 puts every rank on cuda:0
-    (RCCL refuses two ranks on one GPU); the timing logic is the same."""
+def self_launch(args):
+    """--gpus N without a torch.distributed launcher: start N ranks of this script (one per GPU)
+    as child processes and exit with the worst return code.  Nothing here touches a GPU."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def dist_init(args):
+    """One process per GPU.  RCCL (backend "nccl") by default.  Rehearsal overrides for a one-GPU
+    box or a CPU-only host: CTR_BENCH_BACKEND=gloo with CTR_BENCH_SAME_DEVICE=1 puts every rank on
+    cuda:0 (RCCL refuses two ranks on one GPU); the timing logic is the same."""
     import torch
+    if args.dry_run:
+        os.environ["CTR_BENCH_BACKEND"] = "gloo"
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, ws))
     if os.environ.get("CTR_BENCH_SAME_DEVICE") == "1":
         local = 0
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not args.dry_run:
+            torch.cuda.set_device(local)
         backend = os.environ.get("CTR_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-        return dist, rank, ws, local
-    return None, 0, 1, local
+        return dist, rank, ws, local, backend
+    return None, 0, 1, local, None
+
+
+def D_max_over_ranks(v):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    from ctr_reach_amd import distributed as D
+    return D.max_over_ranks(v, device="cpu")
+
+
+def refill_interval_for(steps, cap=64):
+    """Largest divisor of the timed steps that is <= cap: the window then holds whole refill
+    periods (every reset it consumes is precomputed inside it)."""
+    return max(d for d in range(1, min(cap, steps) + 1) if steps % d == 0)
 
 
 def make_actions(env, k, seed):
@@ -140,76 +195,134 @@ def parity_probe(env, cfgd):
 
 
 def cpu_baseline(args, cfgd):
-    """Oracle (C port, OpenMP) on this host: env-steps/s on a bounded sample of the workload."""
+    """Oracle (C port, OpenMP) on this host: env-steps/s on a bounded sample of the workload, with
+    the same staggered episode clocks and auto-resets (2 sampled joint sets + 2 FKs per reset) as
+    the GPU window."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    fkw = dict(integrator=cfgd["integrator"], steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"])
     n = 4096
-    q, _ = oracle.sample_joints(n, seed=args.seed, stream=1)
-    dg = oracle.fk(oracle.sample_joints(n, seed=args.seed, stream=0)[0], integrator=cfgd["integrator"],
-                   steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"])["tip"]
     rng = np.random.default_rng(args.seed + 1)
+    q, _ = oracle.sample_joints(n, seed=args.seed, stream=1)
+    dg = oracle.fk(oracle.sample_joints(n, seed=args.seed, stream=0)[0], **fkw)["tip"]
     hi = np.array([1e-3] * 3 + [np.deg2rad(5)] * 3, np.float32)
-    t = np.zeros(n, np.int32)
-    steps = 0
+    t = rng.integers(0, 150, n).astype(np.int32)
+    steps = resets = 0
+    epoch = 1
     t0 = time.perf_counter()
     while True:
         a = ((rng.random((n, 6)) * 2 - 1) * hi).astype(np.float32)
-        r = oracle.step(q, a, dg, t, 0.020, integrator=cfgd["integrator"], steps_per_m=cfgd["rk4_steps_per_m"],
-                        model=cfgd["model"])
+        r = oracle.step(q, a, dg, t, 0.020, **fkw)
         q, t = r["joints"], r["t"]
-        t[t >= 150] = 0
+        d = np.where(r["done"])[0]
+        if d.size:                                     # CtrReachEnv.reset (ctr_reach_env.py:70-114)
+            epoch += 1
+            qd, _ = oracle.sample_joints(d.size, seed=args.seed, stream=0, epoch=epoch, env_base=int(d[0]))
+            q0, _ = oracle.sample_joints(d.size, seed=args.seed, stream=1, epoch=epoch, env_base=int(d[0]))
+            dg[d] = oracle.fk(qd, **fkw)["tip"]
+            oracle.fk(q0, **fkw)
+            q[d] = q0
+            t[d] = 0
+            resets += d.size
         steps += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
     return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "%d envs x %d steps of oracle/ctr_oracle.c (%s, %s model, fp64), OpenMP %d threads, "
-                      "%.1f s" % (n, steps, cfgd["integrator"], cfgd["model"], threads, el)}
+            "sample": "%d envs x %d steps (%d auto-resets, staggered episode clocks) of oracle/ctr_oracle.c "
+                      "(%s, %s model, fp64), OpenMP %d threads, %.1f s" % (n, steps, resets, cfgd["integrator"],
+                                                                           cfgd["model"], threads, el)}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
     import torch
-    dist, rank, ws, local = dist_init()
+    dist, rank, ws, local, backend = dist_init(args)
+    if args.dry_run:
+        # the multi-rank plumbing without a GPU: every rank reports in, rank 0 prints the count
+        t = torch.ones(1)
+        if dist:
+            dist.all_reduce(t)
+        el = D_max_over_ranks(0.001 * (rank + 1))
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": ws, "ranks_reporting": int(t.item()),
+                              "backend": backend, "max_over_ranks_s": el}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return 0
     from ctr_reach_amd import CtrReachVecEnv
     from ctr_reach_amd import distributed as D
+    from ctr_reach_amd import _abi
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cfgd = CONFIGS[args.config]
     n = args.envs or cfgd["envs"]
-    extra = {} if args.refill_interval is None else {"refill_interval": args.refill_interval}
+    gather = (args.gather == "on") or (args.gather == "auto" and ws > 1)
+    if gather and not dist:
+        raise SystemExit("--gather on needs more than one rank")
+    R = args.refill_interval or refill_interval_for(args.steps)
     systems = [int(s) for s in args.systems.split(",")]
     env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
                          integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"],
-                         select_systems=systems, **extra)
+                         select_systems=systems, refill_interval=R, pack_outputs=gather)
     env.reset()
+    max_steps = env.max_steps_per_episode
+    if not args.no_stagger:
+        # the episode phase of a long-running batch is uniform over [0, max_steps)
+        g = torch.Generator(device="cpu")
+        g.manual_seed(args.seed + 17 + rank)
+        env.t.copy_(torch.randint(0, max_steps, (n,), generator=g, dtype=torch.int32))
     acts = make_actions(env, 8, args.seed + rank)
     stream = torch.cuda.current_stream()
+    works = [None, None]
 
-    for i in range(args.warmup):
+    def one_step(i):
+        k = i & 1
+        if gather and works[k] is not None:
+            works[k].wait()          # the gather that last read this pack buffer (stream-ordered, no host wait)
         env.step_raw(acts[i % len(acts)])
+        if gather:
+            _, works[k] = env.gather_outputs(async_op=True)
+
+    # untimed: one whole episode length (every env passes a time-limit reset), then the warmup
+    for i in range(max_steps + args.warmup):
+        one_step(i)
+    env.refill_pool()                # the window starts on a refill boundary
     torch.cuda.synchronize()
     if args.profile_only:
         for i in range(args.steps):
-            env.step_raw(acts[i % len(acts)])
+            one_step(i)
         torch.cuda.synchronize()
-        return
+        return 0
 
-    # ---- timed region: K whole-job steps (includes auto-resets at their natural rate)
+    # ---- timed region: K whole-job steps, auto-resets and pool refills at their natural rate
+    epoch0 = env.epoch.to(torch.int64).sum()
+    refills0 = env.refills
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        env.step_raw(acts[i % len(acts)])
+        one_step(i)
+    for w in works:
+        if w is not None:
+            w.wait()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    el = D.max_over_ranks(time.perf_counter() - t0,
-                          device=dev if os.environ.get("CTR_BENCH_BACKEND", "nccl") == "nccl" else "cpu")
+    el = D.max_over_ranks(time.perf_counter() - t0, device=dev if backend in (None, "nccl") else "cpu")
+    resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
+    refills = env.refills - refills0
+    resets = resets_local
+    if dist:
+        rt = torch.tensor([resets_local], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(rt)
+        resets = int(rt.item())
     total_steps = n * ws * args.steps
 
     # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset.
@@ -218,7 +331,6 @@ def main():
     # average includes the ~1.5 us launch boundaries and slightly over-states the kernel time.
     j_probe = env.joints.clone()
     flops_env_step, sincos, nfev_mean = fk_work(env, j_probe)
-    from ctr_reach_amd import _abi
     k_iters = max(5, min(args.steps, 32))
     sp = _abi.stream_ptr(stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -233,7 +345,7 @@ def main():
     if rank != 0:
         if dist:
             dist.destroy_process_group()
-        return
+        return 0
     achieved_tf = flops_env_step / (k_ms * 1e-3) / 1e12
     out = {
         "metric": "env-steps/sec at 65 536 parallel 3-tube envs; tip-pos L2 vs CPU ref",
@@ -250,11 +362,18 @@ def main():
         "data": "synthetic: Philox-sampled joints/goals (sample_goal region), uniform actions in the action box",
         "config": {"workload": (cfgd["text"] % n) + ", %s, n_substeps 10, tol 0.020, max 150 steps, "
                                                      "auto-reset" % ("system %d" % systems[0] if len(systems) == 1 else
-                                                                     "systems %s drawn per reset" % args.systems),
+                                                                     "systems %s drawn per reset" % args.systems)
+                   + (", RCCL all-gather of packed tip/reward/done every step" if gather else ""),
                    "integrator": cfgd["integrator"], "model": cfgd["model"],
                    "rk4_steps_per_m": cfgd["rk4_steps_per_m"] if cfgd["integrator"] == "rk4" else None,
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
-                   "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval}},
+                   "process_group": {"backend": backend, "world_size": ws} if dist else None,
+                   "all_gather": {"bytes_per_env": 20, "async": True} if gather else None,
+                   "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval},
+                   "steady_state": {"staggered_t": not args.no_stagger, "untimed_steps_before": max_steps + args.warmup,
+                                    "resets_in_window": resets, "refills_in_window": refills * ws,
+                                    "refills_in_window_per_rank": refills,
+                                    "mean_episode_steps_est": (total_steps / resets) if resets else None}},
         "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": PEAK_FP64_VALU, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_VALU, "traffic": None,
                      "kernel": "k_step", "kernel_ms": k_ms,
@@ -272,14 +391,15 @@ def main():
             t = json.load(fh)
         if t.get("envs") == n and t.get("config", 3) == args.config and systems == [0]:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
-            out["roofline"]["traffic_source"] = "profiles/traffic.json: rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE per k_step"
+            out["roofline"]["traffic_source"] = t.get("source", "profiles/traffic.json")
     if not args.no_cpu_baseline and ws == 1:
         out["parity"] = parity_probe(env, cfgd)
         out["cpu_baseline"] = cpu_baseline(args, cfgd)
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

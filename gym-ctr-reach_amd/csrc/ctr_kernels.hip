@@ -334,6 +334,14 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
     o.error[e] = (float)d;
     uint32_t stat = st.status;
     if (o.nfev) o.nfev[e] = st.nfev;
+    if (o.packed) {
+        // the gather row of this step (distributed.PACK_WIDTH): the pre-reset tip, so a done env
+        // reports where its episode ended
+        float *pk = o.packed + 5 * e;
+        pk[0] = (float)ag[0]; pk[1] = (float)ag[1]; pk[2] = (float)ag[2];
+        pk[3] = reward;
+        pk[4] = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0));
+    }
     // ctr_step_her: the transition goes into the env's HER episode before any auto-reset
     const bool her_closed = her && her_record_lane(*her, e, action, reward, done, obs, ag, tol);
     int32_t t_out = t;

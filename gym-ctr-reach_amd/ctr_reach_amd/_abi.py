@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 8
+CTR_ABI_VERSION = 9
 CTR_MAX_SYSTEMS = 8
 CTR_HER_SCAN_TILE = 1024
 CTR_INTEGRATOR_RK45_SCIPY = 0
@@ -99,6 +99,7 @@ class CtrStepOut(ctypes.Structure):
         ("terminal_achieved", _P),
         ("status", _P),
         ("nfev", _P),
+        ("packed", _P),
     ]
 
 

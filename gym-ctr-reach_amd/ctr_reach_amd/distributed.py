@@ -51,9 +51,26 @@ def all_gather_outputs(packed, group=None, async_op=False):
     import torch
     import torch.distributed as dist
     ws = dist.get_world_size(group)
+    if packed.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo rehearsal of the RCCL path (several ranks on one GPU): gather host copies
+        host = packed.cpu()
+        out = torch.empty((ws * packed.shape[0], packed.shape[1]), dtype=packed.dtype)
+        dist.all_gather_into_tensor(out, host, group=group)
+        out = out.to(packed.device)
+        return (out, _DoneWork()) if async_op else out
     out = torch.empty((ws * packed.shape[0], packed.shape[1]), dtype=packed.dtype, device=packed.device)
     work = dist.all_gather_into_tensor(out, packed.contiguous(), group=group, async_op=async_op)
     return (out, work) if async_op else out
+
+
+class _DoneWork(object):
+    """A completed collective (the synchronous gloo rehearsal path)."""
+
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
 
 
 def max_over_ranks(value, device=None, group=None):

@@ -85,7 +85,7 @@ class CtrReachVecEnv(object):
 
     def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
                  pool_depth=None, refill_interval=64, integrator="rk45_scipy", rk4_steps_per_m=100,
-                 model="compliant", **kwargs):
+                 model="compliant", pack_outputs=False, **kwargs):
         torch = _torch()
         kw = default_kwargs()
         kw.update(kwargs)
@@ -147,6 +147,12 @@ class CtrReachVecEnv(object):
         self.terminal_achieved = torch.zeros((n, 3), dtype=f64, device=dev)
         self.status = torch.zeros(n, dtype=i32, device=dev)
         self.nfev = None
+        # pack_outputs: k_step also writes each step's gather row ([n, 5] f32, distributed.PACK_WIDTH)
+        # into one of two alternating buffers, so gather_outputs() needs no packing launch and one
+        # gather may stay in flight while the next step writes the other buffer
+        self.packed_bufs = [torch.zeros((n, 5), dtype=f32, device=dev) for _ in range(2)] if pack_outputs else None
+        self._packed_k = 0
+        self.refills = 0          # ctr_pool_refill launches so far (bench accounting)
         # reset pool: resets are a pure function of (seed, env id, reset number), so they are
         # precomputed in batches every `refill_interval` steps and consumed by a copy
         if pool_depth is None:
@@ -194,6 +200,7 @@ class CtrReachVecEnv(object):
                                                         p(self.error))
         o.terminal_obs, o.terminal_achieved, o.status = p(self.terminal_obs), p(self.terminal_achieved), p(self.status)
         o.nfev = p(self.nfev)
+        o.packed = p(self.packed_bufs[self._packed_k]) if self.packed_bufs is not None else None
 
     def enable_nfev(self, on=True):
         """Record per-env RHS evaluation counts of the last step (diagnostics / roofline)."""
@@ -225,6 +232,7 @@ class CtrReachVecEnv(object):
         if self.pool_depth:
             rc = self.lib.ctr_pool_refill(self.cfg, self._batch, _abi.stream_ptr(stream))
             _abi.check(rc, "ctr_pool_refill")
+            self.refills += 1
         self._steps_since_refill = 0
 
     def reset(self, goal=None, system=None, mask=None, stream=None):
@@ -273,6 +281,10 @@ class CtrReachVecEnv(object):
         """step() without building Python return values (benchmark / graph capture)."""
         sp = _abi.stream_ptr(stream, self.device.index)
         her = self._her
+        pb = self.packed_bufs
+        if pb is not None:                     # this step writes the buffer the last gather did not
+            self._packed_k ^= 1
+            self._out.packed = pb[self._packed_k].data_ptr()
         if her is not None and her.fused:      # the step records itself into the HER store (ctr_step_her)
             rc = self.lib.ctr_step_her(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
                                        her._h, sp)
@@ -390,16 +402,27 @@ class CtrReachVecEnv(object):
         done, success) packed to 20 B/env and all-gathered over RCCL -> [world * n, 5] float32
         in global-id order.  Not used on the stepping path.  async_op=True returns (out, work)
         and lets the next step() run while the gather is in flight (RCCL's stream); the pack
-        buffers alternate, so one gather may be outstanding per env."""
+        buffers alternate, so one gather may be outstanding per env.
+
+        With ``pack_outputs=True`` the step kernel itself wrote the packed rows (no packing
+        launch); otherwise they are packed here from the step's outputs."""
         import torch
         from . import distributed as D
+        if self.packed_bufs is not None:
+            return D.all_gather_outputs(self.packed_bufs[self._packed_k], group=group, async_op=async_op)
         d = self.done.bool()
         tip = torch.where(d[:, None], self.terminal_achieved, self.achieved_goal) if self.autoreset else self.achieved_goal
         bufs = getattr(self, "_packed", None) or [None, None]
-        k = getattr(self, "_packed_k", 0)
+        k = self._packed_k
         bufs[k] = D.pack_step_outputs(tip, self.reward, d, self.success, out=bufs[k])
         self._packed, self._packed_k = bufs, k ^ 1
         return D.all_gather_outputs(bufs[k], group=group, async_op=async_op)
+
+    def packed_outputs(self):
+        """The last step's packed rows ([n, 5] float32, see gather_outputs); needs pack_outputs=True."""
+        if self.packed_bufs is None:
+            raise RuntimeError("packed_outputs() needs CtrReachVecEnv(..., pack_outputs=True)")
+        return self.packed_bufs[self._packed_k]
 
     def update_goal_tolerance(self, timestep):
         self.goal_tolerance.update(timestep)

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 8
+#define CTR_ABI_VERSION 9
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -157,6 +157,11 @@ typedef struct ctr_step_out_t {
     double   *terminal_achieved; /* [n][3] or NULL: achieved goal of the terminal step           */
     uint32_t *status;            /* [n] or NULL: CTR_STATUS_* bits                               */
     uint32_t *nfev;              /* [n] or NULL: RHS evaluations spent in the step's FK          */
+    float    *packed;            /* [n][5] or NULL: the step's outputs packed for the optional
+                                    all-gather of a single-process trainer: tip x, y, z (float32;
+                                    the terminal achieved goal of a done env), reward,
+                                    done | success << 1 (as a float).  Written by k_step itself,
+                                    so gathering costs no packing launch.                         */
 } ctr_step_out_t;
 
 /* ---------------------------------------------------------------------------------------

@@ -101,3 +101,41 @@ def test_pack_roundtrip():
     a2, r2, d2, s2 = D.unpack_step_outputs(p)
     assert torch.equal(d2, done) and torch.equal(s2, succ) and torch.equal(r2, rew)
     assert torch.allclose(a2, ag.float())
+
+
+def _run_bench(args, env=None, timeout=240):
+    import json
+    import subprocess
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=e, capture_output=True, text=True,
+                       timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_gpus_n_self_launches_ranks():
+    """bench.py --gpus 2 without a launcher starts two ranks itself; they form one process group."""
+    r, out = _run_bench(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out == dict(out, dry_run=True, n_gpus=2, ranks_reporting=2, backend="gloo")
+
+
+def test_bench_refuses_rank_count_mismatch():
+    r, out = _run_bench(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and out is None
+    assert "--gpus 4" in (r.stderr + r.stdout)
+
+
+def test_refill_interval_tiles_the_window():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.refill_interval_for(20) == 20
+    assert bench.refill_interval_for(128) == 64
+    assert bench.refill_interval_for(100) == 50
+    assert bench.refill_interval_for(7) == 7
+    for k in range(1, 300):
+        ri = bench.refill_interval_for(k)
+        assert k % ri == 0 and 1 <= ri <= 64

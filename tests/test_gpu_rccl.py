@@ -50,3 +50,31 @@ def test_gather_outputs_over_rccl(cuda):
         assert torch.equal(out, want)
     finally:
         dist.destroy_process_group()
+
+
+def test_gather_of_kernel_packed_rows_over_rccl(cuda):
+    """pack_outputs=True: k_step writes the gather rows itself (alternating buffers); the RCCL
+    gather of step k, left in flight while step k + 1 runs, returns step k's rows."""
+    import torch
+    import torch.distributed as dist
+    from ctr_reach_amd import CtrReachVecEnv
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    try:
+        n = 4096
+        env = CtrReachVecEnv(n, device=cuda, seed=9, pack_outputs=True, max_steps_per_episode=2)
+        env.reset()
+        rng = np.random.default_rng(3)
+        for _ in range(4):
+            act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * env.action_space.high).astype(np.float32), device=cuda)
+            env.step(act)
+            d = env.done.bool()
+            tip = torch.where(d[:, None], env.terminal_achieved, env.achieved_goal).float()
+            want = torch.cat([tip, env.reward[:, None], (env.done.float() + 2 * env.success.float())[:, None]], 1)
+            out, work = env.gather_outputs(async_op=True)
+            env.step(act)                      # writes the other pack buffer while the gather runs
+            work.wait()
+            torch.cuda.synchronize()
+            assert torch.equal(out, want)
+    finally:
+        dist.destroy_process_group()
