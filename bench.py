@@ -41,10 +41,20 @@ FLOP_ATTEMPT = 1050     # stage combinations 15x18 FMA, y_new 5x18, error 6x18, 
 FLOP_SEGMENT = 150      # select_initial_step arithmetic
 FLOP_RK4_STEP = 252     # RK4: 3 stage inputs 3x18 FMA + y_new 18 x 5 (+ stage sums), per step
 FLOP_STEP_EXTRA = 220   # 10 x set_action (160) + reward/obs (60)
+# configs[1] (rigid model, RK4): the executed work of the matrix-power path (csrc/ctr_device.hpp
+# rigid_step_map / affine_compose / fk_group_rigid4), not the stepped RK4 count it replaces
+FLOP_RIGID_MAP = 258    # per segment: [u]x (45) + P, Q, m of the one-step map (three 3x3 products)
+FLOP_COMPOSE = 63       # one 3x4 affine composition (9 x (mul + 2 fma) + 3 x 3 fma)
+RIGID_TREE = 7          # compositions of the 8-lane group's ordered product (3 shuffle rounds)
 SINCOS_RHS = 3
 PEAK_FP64_VALU = 78.6   # TFLOP/s, MI355X FP64 vector (spec)
 PEAK_HBM = 8000.0       # GB/s (spec)
-BYTES_STEP = 170        # algorithmic bytes per env-step
+# algorithmic bytes per env-step of this layout: reads system 4, joints 24, actions 24, epoch 4,
+# t 4, desired goal 24 (f64) = 84; writes joints 24, achieved goal 24 (f64), t 4, obs 52, reward 4,
+# done 1, success 1, error 4, status 4 = 118.  SURVEY.md 8(d)'s 170 B assumed float32 goals and
+# no system / epoch / status words.  Auto-resets add a pooled reset row (108 B) per reset.
+BYTES_STEP = 84 + 118
+BYTES_RESET = 108
 
 
 def parse():
@@ -160,7 +170,11 @@ def fk_work(env, joints):
     nfev = st["nfev"].double()
     att = (st["nstep"] + st["nrej"]).double()
     seg = st["nseg"].double()
-    if env.integrator == "rk4":
+    if env.integrator == "rk4" and env.model == "rigid":
+        # k_fk's stats[2] counts the square-and-multiply compositions; k_step's 8-lane groups
+        # run the same powers and join the segment maps in RIGID_TREE more compositions
+        per = seg * FLOP_RIGID_MAP + (st["nrej"].double() + RIGID_TREE) * FLOP_COMPOSE
+    elif env.integrator == "rk4":
         per = nfev * FLOP_RHS + att * FLOP_RK4_STEP
     else:
         per = nfev * FLOP_RHS + att * FLOP_ATTEMPT + seg * FLOP_SEGMENT
@@ -302,7 +316,7 @@ def main():
 
     # ---- timed region: K whole-job steps, auto-resets and pool refills at their natural rate
     epoch0 = env.epoch.to(torch.int64).sum()
-    refills0 = env.refills
+    refills0, sweeps0 = env.refills, env.sweeps
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -318,6 +332,7 @@ def main():
     el = D.max_over_ranks(time.perf_counter() - t0, device=dev if backend in (None, "nccl") else "cpu")
     resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
     refills = env.refills - refills0
+    sweeps = env.sweeps - sweeps0
     resets = resets_local
     if dist:
         rt = torch.tensor([resets_local], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
@@ -369,21 +384,27 @@ def main():
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
                    "process_group": {"backend": backend, "world_size": ws} if dist else None,
                    "all_gather": {"bytes_per_env": 20, "async": True} if gather else None,
-                   "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval},
+                   "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,
+                                  "autoreset": "pooled (no miss sweep)" if env.pool_depth >= env.refill_interval
+                                  else "pooled + miss sweep"},
                    "steady_state": {"staggered_t": not args.no_stagger, "untimed_steps_before": max_steps + args.warmup,
                                     "resets_in_window": resets, "refills_in_window": refills * ws,
                                     "refills_in_window_per_rank": refills,
+                                    "miss_sweep_launches_in_window_per_rank": sweeps,
                                     "mean_episode_steps_est": (total_steps / resets) if resets else None}},
         "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": PEAK_FP64_VALU, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_VALU, "traffic": None,
                      "kernel": "k_step", "kernel_ms": k_ms,
                      "flops_per_launch": flops_env_step, "sincos_per_launch": sincos,
                      "nfev_per_env_step": nfev_mean,
+                     "bytes_per_launch_algorithmic": BYTES_STEP * n,
                      "hbm_gbs_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9,
                      "hbm_frac_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9 / PEAK_HBM,
-                     "note": "bound is the FP64 vector pipe: an adaptive RK45 ODE per lane, no GEMM-shaped work for "
-                             "MFMA, ~140 flop/B so HBM is not the limit; peak = MI355X FP64 vector spec; flops = "
-                             "SURVEY 8(d) count from device counters (sincos not priced)"},
+                     "note": ("bound is the FP64 vector pipe: no GEMM-shaped work for MFMA, far above the HBM ridge; "
+                              "peak = MI355X FP64 vector spec; flops from device counters (sincos not priced): " +
+                              ("the EXECUTED work of the rigid matrix-power path (258 flop per segment map + 63 per "
+                               "3x4 composition, incl. the 7 of the 8-lane group product), not the stepped RK4 count"
+                               if cfgd["model"] == "rigid" else "SURVEY 8(d) count"))},
     }
     tr = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tr):
@@ -391,7 +412,8 @@ def main():
             t = json.load(fh)
         if t.get("envs") == n and t.get("config", 3) == args.config and systems == [0]:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
-            out["roofline"]["traffic_source"] = t.get("source", "profiles/traffic.json")
+            out["roofline"]["traffic_source"] = "profiles/traffic.json: " + t.get("note", "")
+            out["roofline"]["traffic_over_algorithmic"] = t.get("bytes_per_launch") / (BYTES_STEP * n)
     if not args.no_cpu_baseline and ws == 1:
         out["parity"] = parity_probe(env, cfgd)
         out["cpu_baseline"] = cpu_baseline(args, cfgd)

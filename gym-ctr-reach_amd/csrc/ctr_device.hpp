@@ -355,6 +355,8 @@ __device__ __forceinline__ void shape_put(ShapeOut *so, double s, const double r
     so->count++;
 }
 
+// nrej: rejected RK45 attempts; fixed-step RK4 never rejects, so with the rigid model (whose
+// segments run as matrix powers) it counts the 3x4 affine compositions of square-and-multiply.
 struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
@@ -882,10 +884,11 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
                     double aq[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, am[3] = {0.0, 0.0, 0.0};
                     int e = left;
                     for (;;) {
-                        if (e & 1) affine_compose(aq, am, rq, rm);      // acc <- acc M^(2^j)
+                        if (e & 1) { affine_compose(aq, am, rq, rm); st.nrej++; }   // acc <- acc M^(2^j)
                         e >>= 1;
                         if (!e) break;
                         affine_square(rq, rm);
+                        st.nrej++;                  // rigid RK4: nrej counts the compositions
                     }
                     double nR[9];
                     #pragma unroll
@@ -1058,9 +1061,10 @@ __device__ __forceinline__ void set_action_lane(const ctr_system_t &sy, bool con
     }
 }
 
-// obs.py:136-164.  Writes obs_dim (13 or 14) floats.
+// obs.py:136-164.  Writes obs_dim (13 or 14) values in float64, the reference's dtype; the env
+// stores them as float32 (rounded once) or float64 (ctr_env_config_t.obs_f64).
 __device__ __forceinline__ void obs_lane(const float q[6], const double dg[3], const double ag[3], double tol,
-                                         int sys, bool multi, bool egocentric, float *out)
+                                         int sys, bool multi, bool egocentric, double *out)
 {
     #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -1068,14 +1072,14 @@ __device__ __forceinline__ void obs_lane(const float q[6], const double dg[3], c
         if (egocentric && i > 0) { b -= (double)q[i - 1]; a -= (double)q[3 + i - 1]; }
         double s, c;
         sincos(a, &s, &c);
-        out[3 * i + 0] = (float)c;
-        out[3 * i + 1] = (float)s;
-        out[3 * i + 2] = (float)b;
+        out[3 * i + 0] = c;
+        out[3 * i + 1] = s;
+        out[3 * i + 2] = b;
     }
     #pragma unroll
-    for (int k = 0; k < 3; ++k) out[9 + k] = (float)(dg[k] - ag[k]);
-    out[12] = (float)tol;
-    if (multi) out[13] = (float)sys;
+    for (int k = 0; k < 3; ++k) out[9 + k] = dg[k] - ag[k];
+    out[12] = tol;
+    out[13] = multi ? (double)sys : 0.0;
 }
 
 // ------------------------------------------------------------------------------------------

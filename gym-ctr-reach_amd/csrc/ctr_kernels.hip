@@ -153,11 +153,27 @@ __device__ __forceinline__ void wave_append(int32_t *counter, int32_t *items_bas
 __device__ __forceinline__ int32_t *miss_counter(const ctr_batch_t &b) { return b.work + (b.work_parity & 1); }
 __device__ __forceinline__ int32_t *miss_items(const ctr_batch_t &b) { return b.work + 2; }
 
-__device__ __forceinline__ void write_obs(float *dst, const float ob[14], bool multi)
+// Row e of an observation buffer: float32 [n][od] or, with cfg.obs_f64, float64 [n][od].
+__device__ __forceinline__ void write_obs(void *base, int64_t e, const double ob[14], bool multi, bool f64)
+{
+    const int od = multi ? 14 : 13;
+    if (f64) {
+        double *dst = static_cast<double *>(base) + od * e;
+        #pragma unroll
+        for (int k = 0; k < 13; ++k) dst[k] = ob[k];
+        if (multi) dst[13] = ob[13];
+    } else {
+        float *dst = static_cast<float *>(base) + od * e;
+        #pragma unroll
+        for (int k = 0; k < 13; ++k) dst[k] = (float)ob[k];
+        if (multi) dst[13] = (float)ob[13];
+    }
+}
+
+__device__ __forceinline__ void obs_to_f32(const double ob[14], float out[14])
 {
     #pragma unroll
-    for (int k = 0; k < 13; ++k) dst[k] = ob[k];
-    if (multi) dst[13] = ob[13];
+    for (int k = 0; k < 14; ++k) out[k] = (float)ob[k];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -325,8 +341,8 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
     const float reward = (d > tol) ? -1.0f : 0.0f;              // ctr_reach_env.py:170
     const bool done = (reward == 0.0f) || (t >= kc.c.max_steps); // :140
     const bool multi = kc.c.n_systems > 1;
-    const int od = multi ? 14 : 13;
-    float obs[14];
+    const bool f64 = kc.c.obs_f64 != 0;
+    double obs[14];
     obs_lane(q, dg, ag, tol, s, multi, kc.c.egocentric != 0, obs);
     o.reward[e] = reward;
     o.done[e] = done ? 1 : 0;
@@ -343,10 +359,14 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
         pk[4] = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0));
     }
     // ctr_step_her: the transition goes into the env's HER episode before any auto-reset
-    const bool her_closed = her && her_record_lane(*her, e, action, reward, done, obs, ag, tol);
+    if (her) {
+        float obf[14];
+        obs_to_f32(obs, obf);
+        her_record_lane(*her, e, action, reward, done, obf, ag, tol);
+    }
     int32_t t_out = t;
     if (autoreset && done) {
-        if (o.terminal_obs) write_obs(o.terminal_obs + od * e, obs, multi);
+        if (o.terminal_obs) write_obs(o.terminal_obs, e, obs, multi, f64);
         if (o.terminal_achieved)
             #pragma unroll
             for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
@@ -375,10 +395,18 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
             b.epoch[e] = r;
             stat |= b.pool_stat[ps];
             obs_lane(q, dg, ag, kc.c.tol, s2, multi, kc.c.egocentric != 0, obs);
-            if (her_closed) her_begin(*her, e, r, obs, ag, dg);     // the next episode starts now
+            if (her) {                                              // the next episode starts now
+                float obf[14];
+                obs_to_f32(obs, obf);
+                her_reopen(*her, e, r, obf, ag, dg);
+            }
             fl.pooled = true;
             fl.pooled_r = r;
             t_out = 0;
+        } else if (autoreset == CTR_AUTORESET_POOLED) {
+            // the caller promised a full pool and launches no sweep: report, keep the env done
+            // (it takes its reset on a later step, once a refill has precomputed it)
+            stat |= CTR_STATUS_POOL_MISS;
         } else {
             fl.miss = true;
         }
@@ -388,7 +416,7 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
     for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = q[i];
     #pragma unroll
     for (int i = 0; i < 3; ++i) b.achieved_goal[3 * e + i] = ag[i];
-    write_obs(o.obs + od * e, obs, multi);
+    write_obs(o.obs, e, obs, multi, f64);
     if (o.status) o.status[e] = stat;
 }
 
@@ -449,8 +477,14 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e);
     }
     if (autoreset) {
-        const int32_t one[1] = {(int32_t)e};
-        wave_append(miss_counter(b), miss_items(b), b.n, fl.miss, one, 1);
+        if (autoreset == CTR_AUTORESET_POOLED) {
+            // no miss sweep follows: zero the next step's miss counter here (this step neither
+            // reads nor appends to either counter)
+            if (blockIdx.x == 0 && threadIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;
+        } else {
+            const int32_t one[1] = {(int32_t)e};
+            wave_append(miss_counter(b), miss_items(b), b.n, fl.miss, one, 1);
+        }
         if (b.pool_depth > 0) {
             const int32_t two[2] = {(int32_t)e, (int32_t)(fl.pooled_r + (uint32_t)b.pool_depth)};
             wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
@@ -538,7 +572,7 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mode, const uint8_t *__restrict__ mask,
                                                     const double *__restrict__ goal,
-                                                    const int32_t *__restrict__ sys_in, float *__restrict__ obs,
+                                                    const int32_t *__restrict__ sys_in, void *__restrict__ obs,
                                                     uint32_t *__restrict__ status, HerK hk, int32_t her_on)
 {
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
@@ -593,12 +627,16 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
             #pragma unroll
             for (int k = 0; k < 3; ++k) b.starting_position[3 * e + k] = ro.ag[k];
         const bool multi = kc.c.n_systems > 1;
-        float ob[14];
+        double ob[14];
         obs_lane(ro.q0, ro.dg, ro.ag, kc.c.tol, ro.sys, multi, kc.c.egocentric != 0, ob);   // :114
-        write_obs(obs + (multi ? 14 : 13) * e, ob, multi);
+        write_obs(obs, e, ob, multi, kc.c.obs_f64 != 0);
         if (status) status[e] |= ro.stat;
         // ctr_step_her: a swept auto-reset miss opens the env's next HER episode here
-        if (her_on && mode == 0 && hk.h.cur_t[e] < 0) her_begin(hk.h, e, r, ob, ro.ag, ro.dg);
+        if (her_on && mode == 0) {
+            float obf[14];
+            obs_to_f32(ob, obf);
+            her_reopen(hk.h, e, r, obf, ro.ag, ro.dg);
+        }
         queue = b.pool_depth > 0;
     }
     if (b.pool_depth > 0) {
@@ -649,6 +687,20 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             b.pool_stat[ps] = ro.stat;
             b.pool_r[ps] = r;
         }
+    }
+}
+
+// Requeue: every env's resets epoch + 1 .. epoch + P that its pool slots do not hold.
+__global__ __launch_bounds__(BLOCK) void k_pool_requeue(ctr_batch_t b)
+{
+    const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const bool in = e < b.n;
+    const uint32_t r = in ? b.epoch[e] : 0u;
+    for (int j = 1; j <= b.pool_depth; ++j) {
+        const uint32_t rr = r + (uint32_t)j;
+        const bool need = in && b.pool_r[(int64_t)(rr % (uint32_t)b.pool_depth) * b.n + e] != rr;
+        const int32_t two[2] = {(int32_t)e, (int32_t)rr};
+        wave_append(b.refill, b.refill + 1, b.refill_cap, need, two, 2);
     }
 }
 
@@ -845,7 +897,10 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
     if (int r = check_batch(b, "ctr_step: batch buffer missing")) return r;
     if (b.n == 0) return 0;
     if (!o.obs || !o.reward || !o.done || !o.success || !o.error) return fail(CTR_EINVAL, "ctr_step: output missing");
+    if (autoreset < CTR_AUTORESET_OFF || autoreset > CTR_AUTORESET_POOLED) return fail(CTR_EINVAL, "ctr_step: bad autoreset");
     if (autoreset && !b.work) return fail(CTR_EINVAL, "ctr_step: autoreset needs batch->work");
+    if (autoreset == CTR_AUTORESET_POOLED && b.pool_depth <= 0)
+        return fail(CTR_EINVAL, "ctr_step: CTR_AUTORESET_POOLED needs a reset pool");
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
@@ -858,7 +913,7 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
     else
         CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
     if (int r = hip_check("ctr_step launch")) return r;
-    if (autoreset) {
+    if (autoreset == CTR_AUTORESET_SWEEP) {
         // misses are rare with a pool: a small grid sweeps the list grid-stride
         const unsigned g = b.pool_depth > 0 ? std::min(grid_for(2 * b.n), 64u) : grid_for(2 * b.n);
         CTR_LAUNCH(k_reset, kc.mode, dim3(g), lane_lds_bytes(kc), s, kc, b, 0, (const uint8_t *)nullptr, (const double *)nullptr,
@@ -879,7 +934,7 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
 }
 
 int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8_t *mask, const double *goal,
-              const int32_t *system, float *obs, uint32_t *status, void *stream)
+              const int32_t *system, void *obs, uint32_t *status, void *stream)
 {
     if (int r = check_cfg(cfg)) return r;
     if (!batch || !obs) return fail(CTR_EINVAL, "ctr_reset: NULL argument");
@@ -908,6 +963,17 @@ int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void 
     if (int r = hip_check("ctr_pool_refill launch")) return r;
     hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.refill);
     return hip_check("ctr_pool_refill clear");
+}
+
+int ctr_pool_requeue(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream)
+{
+    if (int r = check_cfg(cfg)) return r;
+    if (!batch) return fail(CTR_EINVAL, "ctr_pool_requeue: NULL argument");
+    const ctr_batch_t b = *batch;
+    if (int r = check_batch(b, "ctr_pool_requeue: batch buffer missing")) return r;
+    if (b.n == 0 || b.pool_depth == 0) return 0;
+    hipLaunchKernelGGL(k_pool_requeue, dim3(grid_for(b.n)), dim3(BLOCK), 0, (hipStream_t)stream, b);
+    return hip_check("ctr_pool_requeue launch");
 }
 
 int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr_system_t *sys_out,

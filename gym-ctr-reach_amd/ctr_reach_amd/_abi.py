@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 9
+CTR_ABI_VERSION = 10
 CTR_MAX_SYSTEMS = 8
 CTR_HER_SCAN_TILE = 1024
 CTR_INTEGRATOR_RK45_SCIPY = 0
@@ -21,6 +21,10 @@ CTR_STATUS_STEP_UNDERFLOW = 1
 CTR_STATUS_SAMPLER_STUCK = 2
 CTR_STATUS_NAN = 4
 CTR_STATUS_TOO_LONG = 8
+CTR_STATUS_POOL_MISS = 16
+AUTORESET_OFF = 0        # CTR_AUTORESET_OFF
+AUTORESET_SWEEP = 1      # CTR_AUTORESET_SWEEP: pooled resets, misses computed by a sweep launch
+AUTORESET_POOLED = 2     # CTR_AUTORESET_POOLED: every reset comes from the pool, no sweep launch
 CTR_HER_FUTURE = 0
 CTR_HER_FINAL = 1
 CTR_HER_EPISODE = 2
@@ -48,7 +52,7 @@ class CtrEnvConfig(ctypes.Structure):
         ("integrator", ctypes.c_int32),
         ("rk4_steps_per_m", ctypes.c_int32),
         ("model", ctypes.c_int32),
-        ("model_pad", ctypes.c_int32),
+        ("obs_f64", ctypes.c_int32),
         ("tol", ctypes.c_double),
         ("seed", ctypes.c_uint64),
         ("systems", CtrSystem * CTR_MAX_SYSTEMS),
@@ -132,7 +136,7 @@ class CtrHerBatch(ctypes.Structure):
 
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
             "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
-            "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her")
+            "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her", "ctr_pool_requeue")
 
 _lib = None
 
@@ -159,6 +163,7 @@ def load(path=None):
                            ctypes.POINTER(CtrStepOut), i32, _P]
     L.ctr_reset.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P, _P, _P, _P]
     L.ctr_pool_refill.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P]
+    L.ctr_pool_requeue.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P]
     L.ctr_compute_reward.argtypes = [_P, _P, i64, ctypes.c_double, _P, _P]
     L.ctr_domain_params.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P, _P, _P]
     L.ctr_fk_tables.argtypes = [_P, _P, i64, ctypes.POINTER(CtrEnvConfig), _P, _P, _P, _P]
@@ -173,7 +178,7 @@ def load(path=None):
                                ctypes.POINTER(CtrStepOut), i32, ctypes.POINTER(CtrHer), _P]
     for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward",
                "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
-               "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her"):
+               "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her", "ctr_pool_requeue"):
         getattr(L, fn).restype = ctypes.c_int
     if L.ctr_abi_version() != CTR_ABI_VERSION:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))

@@ -4,7 +4,8 @@
 (envs/ctr_reach_env.py:14-17) and exposes reset/step/compute_reward/seed/render/close,
 update_goal_tolerance/get_goal_tolerance/print_parameters, observation_space/action_space
 and ``model.forward_kinematics`` -- backed by a one-env CtrReachVecEnv on the GPU.
-Returned observations are numpy float64 dicts like the reference's.
+Returned observations are numpy float64 dicts like the reference's (computed and stored in
+float64 on the device).
 """
 import numpy as np
 
@@ -104,8 +105,9 @@ class CtrReachEnv(GoalEnvBase):
                   max_steps_per_episode=max_steps_per_episode, n_substeps=n_substeps, evaluation=evaluation,
                   select_systems=select_systems, resample_joints=resample_joints,
                   length_based_sample=length_based_sample, domain_rand=domain_rand)
+        # float64 observations, as the reference returns them (obs.py:153-156)
         self.vec = CtrReachVecEnv(1, device=device, seed=seed, autoreset=False, integrator=integrator,
-                                  rk4_steps_per_m=rk4_steps_per_m, model=model, **kw)
+                                  rk4_steps_per_m=rk4_steps_per_m, model=model, obs_dtype="float64", **kw)
         v = self.vec
         self.select_systems = v.select_systems
         self.ctr_system_parameters = v.ctr_system_parameters
@@ -154,7 +156,7 @@ class CtrReachEnv(GoalEnvBase):
         return self._obs()
 
     def _obs(self):
-        return {"observation": self.vec.obs[0].cpu().numpy().astype(np.float64),
+        return {"observation": self.vec.obs[0].cpu().numpy().copy(),
                 "achieved_goal": self.vec.achieved_goal[0].cpu().numpy().copy(),
                 "desired_goal": self.vec.desired_goal[0].cpu().numpy().copy()}
 

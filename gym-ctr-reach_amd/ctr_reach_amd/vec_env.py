@@ -81,11 +81,15 @@ class CtrReachVecEnv(object):
     Solver kwargs (build-specific): ``integrator`` "rk45_scipy" (default; the
     reference's solve_ivp RK45, bit-for-bit in its step sequence) or "rk4" (fixed step,
     ``rk4_steps_per_m`` equal steps per metre of each segment); ``model`` "compliant" (the
-    reference's torsionally-compliant ODE, model.py:72-117) or "rigid" (GJ -> infinity)."""
+    reference's torsionally-compliant ODE, model.py:72-117) or "rigid" (GJ -> infinity).
+
+    ``obs_dtype``: "float32" (default: what a trainer consumes) or "float64" (the reference's
+    dtype, obs.py:153-156).  The observation is computed in float64 either way; float32 stores it
+    rounded once.  The HER feed records float32 observations."""
 
     def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
                  pool_depth=None, refill_interval=64, integrator="rk45_scipy", rk4_steps_per_m=100,
-                 model="compliant", pack_outputs=False, **kwargs):
+                 model="compliant", pack_outputs=False, obs_dtype="float32", **kwargs):
         torch = _torch()
         kw = default_kwargs()
         kw.update(kwargs)
@@ -124,6 +128,10 @@ class CtrReachVecEnv(object):
                                resample_joints=self.resample_joints, tol=self.goal_tolerance.get_tol(),
                                seed=self.seed_value, integrator=solver[0], rk4_steps_per_m=solver[1],
                                model=solver[2], domain_rand=kw.get("domain_rand", 0.0))
+        if obs_dtype not in ("float32", "float64", torch.float32, torch.float64):
+            raise ValueError("obs_dtype must be float32 or float64")
+        self.obs_dtype = torch.float64 if obs_dtype in ("float64", torch.float64) else torch.float32
+        self.cfg.obs_f64 = int(self.obs_dtype == torch.float64)
         n, dev = self.num_envs, self.device
         f32, f64, i32 = torch.float32, torch.float64, torch.int32
         init = np.asarray(kw["initial_joints"], dtype=np.float64)
@@ -138,12 +146,12 @@ class CtrReachVecEnv(object):
         self.starting_joints = torch.zeros((n, 6), dtype=f32, device=dev) if record_info else None
         self.starting_position = torch.zeros((n, 3), dtype=f64, device=dev) if record_info else None
         # outputs (persistent; step() returns views of these buffers)
-        self.obs = torch.zeros((n, self.obs_dim), dtype=f32, device=dev)
+        self.obs = torch.zeros((n, self.obs_dim), dtype=self.obs_dtype, device=dev)
         self.reward = torch.zeros(n, dtype=f32, device=dev)
         self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.success = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.error = torch.zeros(n, dtype=f32, device=dev)
-        self.terminal_obs = torch.zeros((n, self.obs_dim), dtype=f32, device=dev)
+        self.terminal_obs = torch.zeros((n, self.obs_dim), dtype=self.obs_dtype, device=dev)
         self.terminal_achieved = torch.zeros((n, 3), dtype=f64, device=dev)
         self.status = torch.zeros(n, dtype=i32, device=dev)
         self.nfev = None
@@ -153,15 +161,21 @@ class CtrReachVecEnv(object):
         self.packed_bufs = [torch.zeros((n, 5), dtype=f32, device=dev) for _ in range(2)] if pack_outputs else None
         self._packed_k = 0
         self.refills = 0          # ctr_pool_refill launches so far (bench accounting)
+        self.sweeps = 0           # steps that launched the auto-reset miss sweep (CTR_AUTORESET_SWEEP)
         # reset pool: resets are a pure function of (seed, env id, reset number), so they are
         # precomputed in batches every `refill_interval` steps and consumed by a copy
+        # depth >= the refill interval: every env then finds its next reset in the pool on every
+        # step (CTR_AUTORESET_POOLED, no miss-sweep launch); 108 B per env and slot
         if pool_depth is None:
-            pool_depth = 8 if (self.autoreset and self.resample_joints) else 0
+            pool_depth = max(8, int(refill_interval)) if (self.autoreset and self.resample_joints) else 0
         if pool_depth and not self.resample_joints:
             raise ValueError("the reset pool needs resample_joints=True")
         self.pool_depth = int(pool_depth)
         self.refill_interval = max(1, int(refill_interval))
         self._steps_since_refill = 0
+        # True once a refill has followed a full (re)queue of every env and every refill period
+        # since has taken at most pool_depth steps (pool_depth >= refill_interval)
+        self._pool_full = False
         P = self.pool_depth
         if P:
             self.pool_qd = torch.zeros((P, n, 6), dtype=f32, device=dev)
@@ -212,6 +226,8 @@ class CtrReachVecEnv(object):
         """Bind a device HER replay feed (ctr_reach_amd.her.HerReplayBuffer): every later reset /
         step records into it.  Call before reset()."""
         from .her import HerReplayBuffer
+        if self.obs_dtype != _torch().float32:
+            raise ValueError("the HER feed records float32 observations: use obs_dtype='float32'")
         return HerReplayBuffer(self, slots=slots, n_sampled_goal=n_sampled_goal,
                                goal_selection_strategy=goal_selection_strategy, seed=seed)
 
@@ -225,7 +241,18 @@ class CtrReachVecEnv(object):
             self.cfg.seed = self.seed_value & 0xFFFFFFFFFFFFFFFF
             if self.pool_depth:
                 self.pool_r.zero_()          # precomputed resets belong to the old seed
+                self._requeue_pool()
         return [self.seed_value]
+
+    def _requeue_pool(self, stream=None):
+        """Drop the refill queue and queue every env's next pool_depth resets the pool does not
+        hold (ctr_pool_requeue), then refill: after a seed change or a checkpoint restore."""
+        self.refill[0] = 0
+        rc = self.lib.ctr_pool_requeue(self.cfg, self._batch, _abi.stream_ptr(stream))
+        _abi.check(rc, "ctr_pool_requeue")
+        self._steps_since_refill = 0
+        self.refill_pool(stream)
+        self._pool_full = self.pool_depth >= self.refill_interval
 
     def refill_pool(self, stream=None):
         """Precompute the queued resets into the pool (ctr_pool_refill); asynchronous."""
@@ -233,6 +260,8 @@ class CtrReachVecEnv(object):
             rc = self.lib.ctr_pool_refill(self.cfg, self._batch, _abi.stream_ptr(stream))
             _abi.check(rc, "ctr_pool_refill")
             self.refills += 1
+            if self._steps_since_refill > self.pool_depth:
+                self._pool_full = False      # a period longer than the pool: misses were swept
         self._steps_since_refill = 0
 
     def reset(self, goal=None, system=None, mask=None, stream=None):
@@ -252,12 +281,24 @@ class CtrReachVecEnv(object):
             if bool(bad.any()):
                 raise ValueError("system index out of range")
         self._keep = (g, s, m)   # keep alive until the kernel has consumed them
+        if self.pool_depth and m is None:
+            self.refill[0] = 0   # every env is reset and requeued: older queue entries are moot
         rc = self.lib.ctr_reset(self.cfg, self._batch, _abi.ptr(m), _abi.ptr(g), _abi.ptr(s), _abi.ptr(self.obs),
                                 _abi.ptr(self.status), _abi.stream_ptr(stream))
         _abi.check(rc, "ctr_reset")
         if self._her is not None:
             self._her._open(m, stream)
-        self.refill_pool(stream)
+        if self.pool_depth:
+            # ctr_reset queued the P resets after each reset env's new one; a masked reset keeps
+            # the other envs' pools (the refill below also takes their queued entries)
+            steps = self._steps_since_refill
+            self.refill_pool(stream)
+            if m is None:
+                self._pool_full = self.pool_depth >= self.refill_interval
+            elif steps > self.pool_depth:
+                self._pool_full = False
+        else:
+            self._steps_since_refill = 0
         return self._obs_dict()
 
     def step(self, actions, stream=None):
@@ -285,11 +326,21 @@ class CtrReachVecEnv(object):
         if pb is not None:                     # this step writes the buffer the last gather did not
             self._packed_k ^= 1
             self._out.packed = pb[self._packed_k].data_ptr()
+        mode = _abi.AUTORESET_OFF
+        if self.autoreset:
+            # no done env can miss its pooled reset while at most pool_depth steps have run since
+            # a refill that left every env's next pool_depth resets precomputed (one reset per env
+            # and step): no miss-sweep launch then.  With pool_depth >= refill_interval that holds
+            # on every step once reset() (or a requeue) has filled the pool.
+            if self._pool_full and self._steps_since_refill < self.pool_depth:
+                mode = _abi.AUTORESET_POOLED
+            else:
+                mode = _abi.AUTORESET_SWEEP
+                self.sweeps += 1
         if her is not None and her.fused:      # the step records itself into the HER store (ctr_step_her)
-            rc = self.lib.ctr_step_her(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset),
-                                       her._h, sp)
+            rc = self.lib.ctr_step_her(self.cfg, self._batch, _abi.ptr(actions), self._out, mode, her._h, sp)
         else:
-            rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, int(self.autoreset), sp)
+            rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, mode, sp)
         if rc:
             _abi.check(rc, "ctr_step")
         if her is not None and not her.fused:  # ctr_her_record from the step's outputs
@@ -431,18 +482,32 @@ class CtrReachVecEnv(object):
         return self.goal_tolerance.get_tol()
 
     # ------------------------------------------------------------------ checkpoint
+    _STATE_KEYS = ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs")
+
     def state_dict(self):
-        keys = ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch")
-        sd = {k: getattr(self, k).clone() for k in keys}
+        sd = {k: getattr(self, k).clone() for k in self._STATE_KEYS}
         sd["seed"] = self.seed_value
         sd["tol"] = self.goal_tolerance.get_tol()
         return sd
 
     def load_state_dict(self, sd):
-        for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch"):
-            getattr(self, k).copy_(sd[k])
-        self.seed(sd["seed"])
+        """Restore the batch state.  The reset pool is re-keyed to the restored reset numbers
+        (queue dropped, next pool_depth resets requeued and refilled), the auto-reset miss
+        counters are cleared, and a bound HER store drops its open episodes and opens new ones
+        from the restored state (the finished episodes it holds stay sampleable)."""
+        for k in self._STATE_KEYS:
+            if k in sd:
+                getattr(self, k).copy_(sd[k])
         self.goal_tolerance.current_tol = sd["tol"]
+        self.cfg.tol = float(sd["tol"])
+        self.work.zero_()
+        self._batch.work_parity = 0
+        self.seed_value = int(sd["seed"])
+        self.cfg.seed = self.seed_value & 0xFFFFFFFFFFFFFFFF
+        if self.pool_depth:
+            self._requeue_pool()
+        if self._her is not None:
+            self._her._open(None, None)
 
     def close(self):
         pass

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 9
+#define CTR_ABI_VERSION 10
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -57,6 +57,20 @@ extern "C" {
 #define CTR_STATUS_NAN            4u   /* model.py:69 assert not any(isnan(r)) */
 #define CTR_STATUS_TOO_LONG       8u   /* fixed-step RK4: a segment needs > 2^20 steps (joints far
                                            outside the action box); the tip is NaN          */
+#define CTR_STATUS_POOL_MISS     16u   /* CTR_AUTORESET_POOLED step: a done env found no pooled
+                                           reset (the caller's no-miss promise was broken); the
+                                           env stays done and is reset on a later step       */
+
+/* ctr_step / ctr_step_her autoreset argument */
+#define CTR_AUTORESET_OFF    0   /* done environments are left as they are                          */
+#define CTR_AUTORESET_SWEEP  1   /* done environments are reset in the same call: from the reset pool
+                                    if it holds their next reset, else by a miss sweep (a second,
+                                    small launch that computes the missing resets)                  */
+#define CTR_AUTORESET_POOLED 2   /* as SWEEP, but the caller guarantees every done environment finds
+                                    its reset in the pool, so no sweep is launched: true when at most
+                                    pool_depth steps have run since the last ctr_pool_refill (each
+                                    step takes at most one reset per environment, and a refill leaves
+                                    every environment's next pool_depth resets precomputed)          */
 
 /* One 3-tube system (index 0 = innermost tube), derived on the host from the
  * registration kwargs exactly as Tube.__init__ (envs/CTR_Python/Tube.py:7-19):
@@ -98,7 +112,10 @@ typedef struct ctr_env_config_t {
     int32_t integrator;         /* CTR_INTEGRATOR_*                                      */
     int32_t rk4_steps_per_m;    /* RK4 only: steps per metre of arclength (> 0)          */
     int32_t model;              /* CTR_MODEL_*                                           */
-    int32_t model_pad;
+    int32_t obs_f64;            /* observation buffers (ctr_step_out_t.obs / terminal_obs,
+                                   ctr_reset's obs): 0 = float32 [n][obs_dim], 1 = float64
+                                   [n][obs_dim], the reference's dtype (obs.py:153-156).
+                                   The values are computed in float64 either way.        */
     double  tol;                /* goal_tolerance.get_tol()                              */
     uint64_t seed;              /* Philox key for resets                                 */
     ctr_system_t systems[CTR_MAX_SYSTEMS];
@@ -148,12 +165,14 @@ typedef struct ctr_batch_t {
 
 /* Per-step outputs (device). obs_dim = 13, or 14 when n_systems > 1 (obs.py:153-156). */
 typedef struct ctr_step_out_t {
-    float    *obs;               /* [n][obs_dim]   observation after the step (after auto-reset) */
+    void     *obs;               /* [n][obs_dim]   observation after the step (after auto-reset);
+                                    float32, or float64 with cfg->obs_f64                         */
     float    *reward;            /* [n]            0 or -1                                       */
     uint8_t  *done;              /* [n]                                                          */
     uint8_t  *success;           /* [n]            info['is_success']                            */
     float    *error;             /* [n]            info['error'] = ||dg - ag||                   */
-    float    *terminal_obs;      /* [n][obs_dim] or NULL: pre-reset observation of done envs     */
+    void     *terminal_obs;      /* [n][obs_dim] or NULL: pre-reset observation of done envs
+                                    (the dtype of obs)                                           */
     double   *terminal_achieved; /* [n][3] or NULL: achieved goal of the terminal step           */
     uint32_t *status;            /* [n] or NULL: CTR_STATUS_* bits                               */
     uint32_t *nfev;              /* [n] or NULL: RHS evaluations spent in the step's FK          */
@@ -264,7 +283,9 @@ const char *ctr_last_error(void);
 
 /* Batched Model.forward_kinematics: joints [n][6] f32 -> tip [n][3] f64.
  * sys_idx: [n] or NULL (all system 0).  stats: [n][4] or NULL = {RHS evaluations, accepted
- * RK steps, rejected RK attempts, integrated segments}.  status: [n] or NULL.  (device) */
+ * RK steps, rejected RK attempts, integrated segments}; fixed-step RK4 never rejects, and with
+ * the rigid model stats[2] counts the 3x4 affine compositions of the segments' matrix powers
+ * (the executed work of that path).  status: [n] or NULL.  (device) */
 int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg,
            double *tip, uint32_t *stats, uint32_t *status, void *stream);
 
@@ -297,8 +318,8 @@ int ctr_set_action(const ctr_env_config_t *cfg, float *joints, const int32_t *sy
                    const float *actions, int64_t n, void *stream);
 
 /* One CtrReachEnv.step for every environment of the batch; actions [n][6] f32 (device).
- * autoreset != 0: done environments are reset in the same call (VecEnv semantics) and
- * their pre-reset observation goes to out->terminal_obs. */
+ * autoreset (CTR_AUTORESET_*) != 0: done environments are reset in the same call (VecEnv
+ * semantics) and their pre-reset observation goes to out->terminal_obs. */
 int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float *actions,
              const ctr_step_out_t *out, int32_t autoreset, void *stream);
 
@@ -306,12 +327,17 @@ int ctr_step(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const float 
  * goal [n][3] or NULL (sample a goal), system [n] or NULL (sample uniformly).
  * Writes the reset observation to obs [n][obs_dim]. */
 int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8_t *mask,
-              const double *goal, const int32_t *system, float *obs, uint32_t *status, void *stream);
+              const double *goal, const int32_t *system, void *obs, uint32_t *status, void *stream);
 
 /* Precompute the resets queued in batch->refill (queued by ctr_step when a pooled reset is
  * consumed, and by ctr_reset for the P resets after the one it computes), then clear the
  * queue.  Call it every few steps; it is a no-op when the queue is empty. */
 int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
+
+/* Queue every environment's next pool_depth resets (epoch + 1 .. epoch + P) that its pool slots
+ * do not hold, e.g. after the batch state was restored from a checkpoint or the seed changed;
+ * the next ctr_pool_refill computes them. */
+int ctr_pool_requeue(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
 
 /* The tube table each environment's current episode uses (Model.current_sys_parameters,
  * model.py:13,20-28): with domain randomisation the episode's re-sampled table, else the

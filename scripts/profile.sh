@@ -18,4 +18,9 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ
     python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc4.log 2>&1 || echo "pmc4 failed (counter names?)"
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS --output-format csv -d $OUT/pmc_mix -o run -- \
     python3 bench.py --steps 10 --warmup 2 --profile-only > $OUT/pmc5.log 2>&1 || echo "pmc5 failed (counter names?)"
+# FETCH_SIZE / WRITE_SIZE calibration for k_step's access shapes (tools/traffic_probe.hip)
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/probe_fetch -o run -- \
+    ./tools/traffic_probe > $OUT/probe1.log 2>&1 || exit 6
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/probe_write -o run -- \
+    ./tools/traffic_probe > $OUT/probe2.log 2>&1 || exit 7
 find $OUT -name "*.csv" | head -50

@@ -168,3 +168,61 @@ def _check_pool_misses(cuda, fused):
         np.testing.assert_array_equal(got["obs"][i], row["obs"])
         np.testing.assert_array_equal(got["next_obs"][i], row["next_obs"])
         assert got["reward"][i] == row["reward"]
+
+
+def test_fused_and_unfused_recording_write_identical_stores(cuda, oracle_mod):
+    """The same seeds and actions through ctr_step_her (recording inside k_step) and through
+    ctr_step + ctr_her_record (a second launch reading the step outputs): every store buffer is
+    byte-equal, pool misses (a one-deep pool, never refilled) included."""
+    for envkw in ({}, dict(pool_depth=1, refill_interval=100000)):
+        stores = []
+        for fused in (True, False):
+            env, her, rec = _run(cuda, n=40, steps=30, fused=fused, **envkw)
+            stores.append({k: getattr(her, k).cpu().numpy().copy()
+                           for k in ("state", "step_rows", "len", "epoch", "dg", "tol", "cur_t", "cur_epoch")})
+        for k in stores[0]:
+            np.testing.assert_array_equal(stores[0][k].view(np.uint8), stores[1][k].view(np.uint8), err_msg=k)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_reset_opens_episode_when_none_was_open(cuda, fused):
+    """One rule on every path: every auto-reset opens the env's next episode, also for an env
+    that had no open episode before the step (cur_t = -1), whether its reset comes from the
+    pool (first reset after the refill) or from the miss sweep (the one-deep pool is empty)."""
+    import torch
+    from ctr_reach_amd import CtrReachVecEnv
+    n = 128
+    env = CtrReachVecEnv(n, device=cuda, seed=4, max_steps_per_episode=2, goal_tolerance_parameters=GTP,
+                         pool_depth=1, refill_interval=100000)
+    env.goal_tolerance.current_tol = 1e-12
+    her = env.enable_her(slots=3)
+    her.fused = fused
+    env.reset()
+    z = torch.zeros((n, 6), device=cuda)
+    for cycle in range(2):                          # cycle 0: pooled reset; cycle 1: pool miss -> sweep
+        env.step(z)
+        her.cur_t[: n // 2] = -1                   # these envs have no open episode at the done step
+        env.step(z)
+        torch.cuda.synchronize()
+        assert env.done.bool().all() and (env.t.cpu().numpy() == 0).all()
+        assert (her.cur_t.cpu().numpy() == 0).all(), cycle
+        np.testing.assert_array_equal(her.cur_epoch.cpu().numpy(), env.epoch.cpu().numpy().astype(np.uint32))
+    assert env.sweeps > 0
+
+
+def test_step_her_rejects_mismatched_store(cuda):
+    from ctr_reach_amd import CtrReachVecEnv, _abi
+    import torch
+    env = CtrReachVecEnv(16, device=cuda, seed=1)
+    her = env.enable_her()
+    env.reset()
+    a = torch.zeros((16, 6), device=cuda)
+    her._h.t_max = env.max_steps_per_episode + 1
+    rc = env.lib.ctr_step_her(env.cfg, env._batch, _abi.ptr(a), env._out, _abi.AUTORESET_POOLED, her._h,
+                              _abi.stream_ptr())
+    assert rc == -1 and b"t_max" in env.lib.ctr_last_error()
+    her._h.t_max = env.max_steps_per_episode
+    her._h.env_base = 5
+    rc = env.lib.ctr_step_her(env.cfg, env._batch, _abi.ptr(a), env._out, _abi.AUTORESET_POOLED, her._h,
+                              _abi.stream_ptr())
+    assert rc == -1 and b"env_base" in env.lib.ctr_last_error()

@@ -2,7 +2,8 @@
 
 Bars (stated per test): joints / reward / done / success / RNG draws bit-exact; tips
 within 1e-10 m of the reference fixtures (fp64 kernel; north_star bar is 1e-4 m); observation
-float32 within 1e-6 of the reference's float64 observation.
+stored as float32 within 1e-6 of the reference's float64 observation, stored as float64
+(obs_dtype="float64", the facade's) at the float64 bar of _obs_within_bar.
 """
 import os
 
@@ -65,14 +66,32 @@ def test_fk_large_batch_vs_oracle(cuda, oracle_mod):
     assert (st["nfev"].cpu().numpy() == ref["nfev"]).mean() > 0.999
 
 
+def _obs_within_bar(got, want, dtype):
+    """The observation bar.  float32 storage: the reference's float64 values rounded once, so
+    within 1e-6 absolute (every component is bounded by 1 in magnitude; f32 spacing there is
+    <= 6e-8).  float64 storage: the trig and extension parts within 1e-15 (the device sincos
+    against numpy's, <= 2 ulp), the goal offset dg - ag within TIP_TOL (the tips' bar), the
+    tolerance (and system index) exact."""
+    got, want = np.asarray(got), np.asarray(want)
+    if dtype == "float32":
+        assert got.dtype == np.float32
+        assert np.abs(got - want).max() < 1e-6
+        return
+    assert got.dtype == np.float64
+    assert np.abs(got[:, :9] - want[:, :9]).max() < 1e-15
+    assert np.abs(got[:, 9:12] - want[:, 9:12]).max() < TIP_TOL
+    np.testing.assert_array_equal(got[:, 12:], want[:, 12:])
+
+
+@pytest.mark.parametrize("obs_dtype", ["float32", "float64"])
 @pytest.mark.parametrize("name,select", [("step_single.npz", [0]), ("step_multi.npz", [0, 1, 2, 3])])
-def test_step_matches_reference_fixtures(golden_dir, cuda, name, select):
+def test_step_matches_reference_fixtures(golden_dir, cuda, name, select, obs_dtype):
     import torch
     d = _d(golden_dir, name)
     for ca in (False, True):
         m = d["constrain_alpha"] == ca
         n = int(m.sum())
-        env = _env(cuda, n, select_systems=select, constrain_alpha=ca, autoreset=False)
+        env = _env(cuda, n, select_systems=select, constrain_alpha=ca, autoreset=False, obs_dtype=obs_dtype)
         env.joints.copy_(torch.tensor(d["joints_in"][m]))
         env.desired_goal.copy_(torch.tensor(d["desired_goal"][m]))
         env.t.copy_(torch.tensor(d["t_in"][m].astype(np.int32)))
@@ -86,7 +105,7 @@ def test_step_matches_reference_fixtures(golden_dir, cuda, name, select):
             torch.cuda.synchronize()
             np.testing.assert_array_equal(env.joints.cpu().numpy()[k], d["joints_out"][m][k].astype(np.float32))
             assert np.abs(env.achieved_goal.cpu().numpy()[k] - d["achieved_goal"][m][k]).max() < TIP_TOL
-            assert np.abs(obs["observation"].cpu().numpy()[k] - d["observation"][m][k]).max() < 1e-6
+            _obs_within_bar(obs["observation"].cpu().numpy()[k], d["observation"][m][k], obs_dtype)
             np.testing.assert_array_equal(rew.cpu().numpy()[k], d["reward"][m][k].astype(np.float32))
             np.testing.assert_array_equal(done.cpu().numpy()[k], d["done"][m][k])
             np.testing.assert_array_equal(info["is_success"].cpu().numpy()[k], d["is_success"][m][k])
@@ -223,6 +242,34 @@ def test_compute_reward_device_vs_numpy(cuda):
     np.testing.assert_array_equal(r_dev.cpu().numpy(), r_np.astype(np.float32))
 
 
+def test_facade_step_observation_vs_reference(golden_dir, cuda):
+    """The single-env facade (CtrReachEnv.step) on the reference's recorded steps: float64
+    observation dicts at the float64 bar of _obs_within_bar, reward / done / success exact."""
+    import torch
+    from ctr_reach_amd import make
+    d = _d(golden_dir, "step_single.npz")
+    rows = np.arange(0, len(d["t_in"]), 7)
+    envs = {}
+    got = []
+    for i in rows:
+        ca = bool(d["constrain_alpha"][i])
+        if ca not in envs:
+            envs[ca] = make("CTR-Reach-v0", device=cuda, constrain_alpha=ca)
+            envs[ca].reset()
+        env = envs[ca]
+        env.goal_tolerance.current_tol = float(d["tol"][i])
+        env.vec.joints.copy_(torch.tensor(d["joints_in"][i][None]))
+        env.vec.t.fill_(int(d["t_in"][i]))
+        env.vec.desired_goal.copy_(torch.tensor(d["desired_goal"][i][None]))
+        env.desired_goal = d["desired_goal"][i].copy()
+        obs, reward, done, info = env.step(d["action"][i])
+        assert isinstance(obs["observation"], np.ndarray) and obs["observation"].dtype == np.float64
+        assert reward == d["reward"][i] and done == bool(d["done"][i]) and info["is_success"] == d["is_success"][i]
+        assert abs(info["error"] - d["error"][i]) < TIP_TOL
+        got.append(obs["observation"])
+    _obs_within_bar(np.array(got), d["observation"][rows], "float64")
+
+
 def test_facade_gym_surface(cuda):
     from ctr_reach_amd import make
     env = make("CTR-Reach-v0", device=cuda)
@@ -252,11 +299,13 @@ def test_facade_gym_surface(cuda):
         env.close()
 
 
-@pytest.mark.parametrize("depth,interval,rand", [(4, 8, 0.0), (1, 1000, 0.0), (2, 3, 0.0), (4, 8, 0.05)])
+@pytest.mark.parametrize("depth,interval,rand", [(4, 8, 0.0), (1, 1000, 0.0), (2, 3, 0.0), (4, 8, 0.05),
+                                                  (8, 4, 0.0), (5, 5, 0.05)])
 def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
     """Pooled auto-resets (precomputed ahead of time, consumed by a copy; including pool misses
     that fall back to the synchronous path) give bit-identical trajectories to computing every
-    reset at the step that needs it: a reset is a pure function of (seed, env id, reset number)."""
+    reset at the step that needs it: a reset is a pure function of (seed, env id, reset number).
+    depth >= interval: every step runs CTR_AUTORESET_POOLED (no miss sweep launched at all)."""
     import torch
     n = 4096
     kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3], domain_rand=rand)
@@ -272,7 +321,83 @@ def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
         torch.cuda.synchronize()
         for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs", "terminal_obs"):
             np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(), err_msg=k)
+        assert not (b.status.cpu().numpy() & 16).any()          # CTR_STATUS_POOL_MISS never raised
     assert (a.epoch.cpu().numpy() >= 4).all()
+    assert a.sweeps == 13                                         # no pool: every step sweeps
+    if depth >= interval:
+        assert b.sweeps == 0
+    else:
+        assert b.sweeps > 0
+
+
+def test_pooled_autoreset_broken_promise_is_flagged(cuda):
+    """CTR_AUTORESET_POOLED on a pool that does NOT hold the next resets (the caller's promise
+    broken): done envs are flagged CTR_STATUS_POOL_MISS and keep their state (no reset, t counts
+    on); with CTR_AUTORESET_SWEEP the same step resets them through the miss sweep."""
+    import torch
+    from ctr_reach_amd import _abi
+    n = 512
+    env = _env(cuda, n, seed=3, max_steps_per_episode=2, pool_depth=4, refill_interval=4)
+    env.goal_tolerance.current_tol = 1e-12
+    env.reset()
+    env.step(torch.zeros((n, 6), device=cuda))
+    env.pool_r.zero_()                                  # the pool no longer holds anything
+    ep0 = env.epoch.clone()
+    a = torch.zeros((n, 6), device=cuda)
+    rc = env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(a), env._out, _abi.AUTORESET_POOLED, _abi.stream_ptr())
+    _abi.check(rc, "ctr_step")
+    env._batch.work_parity ^= 1
+    torch.cuda.synchronize()
+    assert env.done.bool().all()
+    assert ((env.status.cpu().numpy() & _abi.CTR_STATUS_POOL_MISS) != 0).all()
+    assert torch.equal(env.epoch, ep0) and (env.t.cpu().numpy() == 2).all()
+    rc = env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(a), env._out, _abi.AUTORESET_SWEEP, _abi.stream_ptr())
+    _abi.check(rc, "ctr_step")
+    env._batch.work_parity ^= 1
+    torch.cuda.synchronize()
+    assert (env.t.cpu().numpy() == 0).all() and torch.equal(env.epoch, ep0 + 1)
+    assert not (env.status.cpu().numpy() & _abi.CTR_STATUS_POOL_MISS).any()
+    # a bad mode is an argument error
+    assert env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(a), env._out, 3, _abi.stream_ptr()) == -1   # CTR_EINVAL
+
+
+@pytest.mark.parametrize("her_on", [False, True])
+def test_state_dict_roundtrip_replays_exactly(cuda, her_on):
+    """save -> step -> load -> step reproduces the same trajectory bit for bit (the pool is
+    re-keyed to the restored reset numbers; auto-resets inside both windows); with a HER store
+    the open episodes are dropped on load and reopened from the restored state."""
+    import torch
+    n = 2048
+    env = _env(cuda, n, seed=21, max_steps_per_episode=5, refill_interval=3)
+    env.goal_tolerance.current_tol = 0.03
+    her = env.enable_her(slots=3) if her_on else None
+    env.reset()
+    rng = np.random.default_rng(12)
+    acts = [torch.tensor((rng.uniform(-1, 1, (n, 6)) * env.action_space.high).astype(np.float32), device=cuda)
+            for _ in range(9)]
+    for a in acts[:4]:
+        env.step(a)
+    sd = env.state_dict()
+    keys = ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs", "reward", "done")
+
+    def run():
+        out = []
+        for a in acts[4:]:
+            env.step(a)
+            out.append({k: getattr(env, k).cpu().numpy().copy() for k in keys})
+        return out
+    first = run()
+    env.load_state_dict(sd)
+    if her_on:
+        torch.cuda.synchronize()
+        assert (her.cur_t.cpu().numpy() == 0).all()
+        np.testing.assert_array_equal(her.cur_epoch.cpu().numpy(), sd["epoch"].cpu().numpy().astype(np.uint32))
+    second = run()
+    assert int((torch.tensor(second[-1]["epoch"]) - sd["epoch"].cpu()).sum()) > n   # resets in the window
+    for x, y in zip(first, second):
+        for k in keys:
+            np.testing.assert_array_equal(x[k], y[k], err_msg=k)
+    assert env.sweeps == 0
 
 
 @pytest.mark.parametrize("n", [1, 63, 65, 257])

@@ -3,9 +3,11 @@
 Writes:
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_pmc.json           per-kernel PMC averages (per launch)
+  profiles/<tag>_traffic_calibration.json  FETCH_SIZE / WRITE_SIZE against known byte counts in
+                                    k_step's access shapes (tools/traffic_probe.hip)
   profiles/traffic.json             HBM bytes per k_step launch for bench.py's roofline.traffic:
-                                    FETCH_SIZE x 2 (gfx950 reports half of wide reads,
-                                    MI355X_MICROARCH.md HBM section) + WRITE_SIZE, KiB -> bytes
+                                    FETCH_SIZE and WRITE_SIZE scaled by the calibrated factors
+                                    (KiB -> bytes)
 """
 import collections
 import csv
@@ -45,15 +47,47 @@ with open(os.path.join(dst, tag + "_pmc.json"), "w") as fh:
 step = [k for k in out if "k_step" in k]
 stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
 avg_ns = {kname(r["Name"]): float(r["AverageNs"]) for r in stats}
+# FETCH_SIZE / WRITE_SIZE calibration on known byte counts in k_step's own access shapes
+# (tools/traffic_probe.hip, scripts/profile.sh passes probe_fetch / probe_write)
+cal = None
+probe = {}
+for sub, ctr in (("probe_fetch", "FETCH_SIZE"), ("probe_write", "WRITE_SIZE")):
+    f = os.path.join(src, sub, "run_counter_collection.csv")
+    if os.path.exists(f):
+        acc = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == ctr:
+                acc[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024)
+        probe[ctr] = {k: sum(v) / len(v) for k, v in acc.items()}
+if "FETCH_SIZE" in probe and "WRITE_SIZE" in probe:
+    logf = os.path.join(src, "probe1.log")
+    known = json.loads([ln for ln in open(logf) if ln.startswith("{")][-1])
+    pf, pw = probe["FETCH_SIZE"], probe["WRITE_SIZE"]
+    cal = {"tool": "tools/traffic_probe.hip (scripts/profile.sh)", "known_bytes": known,
+           "fetch_size_bytes": {k: pf[k] for k in ("k_rows_cold", "k_rows_warm", "k_stream_cold") if k in pf},
+           "write_size_bytes": {k: pw[k] for k in ("k_rows_write", "k_rows_cold") if k in pw},
+           "read_factor_rows_cold": known["read_bytes_known"] / pf["k_rows_cold"],
+           "read_factor_rows_warm": known["read_bytes_known"] / pf["k_rows_warm"],
+           "read_factor_stream16": known["stream_bytes_known"] / pf["k_stream_cold"],
+           "write_factor_rows": known["write_bytes_known"] / pw["k_rows_write"],
+           "write_factor_sink": known["sink_bytes"] / pw["k_rows_cold"]}
+    with open(os.path.join(dst, tag + "_traffic_calibration.json"), "w") as fh:
+        json.dump(cal, fh, indent=1)
+    print(json.dumps(cal, indent=1))
 if step:
     d = out[step[0]]
     fetch = d.get("FETCH_SIZE", 0.0) * 1024
     write = d.get("WRITE_SIZE", 0.0) * 1024
     envs = 65536
-    t = {"envs": envs, "kernel": step[0], "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
-         "bytes_per_launch": 2 * fetch + write,
-         "note": "FETCH_SIZE doubled per the gfx950 calibration for wide reads; k_step reads 4-8 B/lane "
-                 "AoS rows, for which the counter is uncalibrated",
+    rf = cal["read_factor_rows_warm"] if cal else 2.0
+    wf = cal["write_factor_rows"] if cal else 1.0
+    t = {"envs": envs, "kernel": step[0], "fetch_size_bytes_raw": fetch, "write_size_bytes_raw": write,
+         "read_factor": rf, "write_factor": wf,
+         "bytes_per_launch": rf * fetch + wf * write,
+         "read_bytes": rf * fetch, "write_bytes": wf * write,
+         "note": ("FETCH_SIZE x read_factor + WRITE_SIZE x write_factor, the factors measured on known byte "
+                  "counts in k_step's own row-load / row-store shapes (%s_traffic_calibration.json)" % tag)
+         if cal else "FETCH_SIZE doubled per the gfx950 calibration for wide reads (uncalibrated here)",
          "avg_ns_rocprof": avg_ns.get(step[0])}
     with open(os.path.join(dst, "traffic.json"), "w") as fh:
         json.dump(t, fh, indent=1)
