@@ -46,6 +46,7 @@ __device__ __forceinline__ void cswap(double &a, double &b, int &ia, int &ib)
     a = ta; b = tb; ia = ja; ib = jb;
 }
 
+template <int STRIDE = CTR_BLOCK>      // LDS column stride of end_lds (lanes of the workgroup)
 __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double beta[3], double *end_lds)
 {
 #pragma clang fp contract(off)
@@ -107,7 +108,7 @@ __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double be
     #pragma unroll
     for (int k = 0; k < 9; ++k) {         // :46-55 (adding a zero gap is an exact no-op)
         cum += len[k];
-        end_lds[k * CTR_BLOCK] = cum + bmin;
+        end_lds[k * STRIDE] = cum + bmin;
         sg.kept |= ((len[k] != 0.0) && (cum + bmin > 0.0)) ? (1u << k) : 0u;
     }
     return sg;
