@@ -830,6 +830,16 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             b.pool_r[ps] = r;
         }
     }
+    // the last workgroup to finish clears the queue (every workgroup read the count at its
+    // start): a ticket at refill[1 + 2 cap] instead of a clearing launch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t *ticket = b.refill + 1 + 2 * b.refill_cap;
+        if (atomicAdd(ticket, 1) == (int32_t)gridDim.x - 1) {
+            b.refill[0] = 0;
+            *ticket = 0;
+        }
+    }
 }
 
 // Requeue: every env's resets epoch + 1 .. epoch + P that its pool slots do not hold.
@@ -866,11 +876,6 @@ __global__ __launch_bounds__(BLOCK) void k_domain_params(KCfg kc, ctr_batch_t b,
     }
     if (sys_out) sys_out[e] = sy;
     if (raw_out) raw_out[e] = raw;
-}
-
-__global__ __launch_bounds__(64) void k_clear_counter(int32_t *counter)
-{
-    if (threadIdx.x == 0 && blockIdx.x == 0) counter[0] = 0;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_reward(const double *__restrict__ ag, const double *__restrict__ dg,
@@ -1141,9 +1146,7 @@ int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void 
     hipStream_t s = (hipStream_t)stream;
     // grid covers one entry per env (2 lanes each); larger queues are swept grid-stride
     CTR_LAUNCH(k_refill, kc.mode, dim3(grid_for(2 * b.n)), lane_lds_bytes(kc), s, kc, b);
-    if (int r = hip_check("ctr_pool_refill launch")) return r;
-    hipLaunchKernelGGL(k_clear_counter, dim3(1), dim3(64), 0, s, b.refill);
-    return hip_check("ctr_pool_refill clear");
+    return hip_check("ctr_pool_refill launch");
 }
 
 int ctr_pool_requeue(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream)

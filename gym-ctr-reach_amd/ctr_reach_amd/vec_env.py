@@ -186,7 +186,7 @@ class CtrReachVecEnv(object):
             self.pool_r = torch.zeros((P, n), dtype=i32, device=dev)
             self.pool_stat = torch.zeros((P, n), dtype=i32, device=dev)
             self.refill_cap = n * (P + self.refill_interval)
-            self.refill = torch.zeros(1 + 2 * self.refill_cap, dtype=i32, device=dev)
+            self.refill = torch.zeros(2 + 2 * self.refill_cap, dtype=i32, device=dev)   # count, pairs, ticket
         else:
             self.pool_qd = self.pool_dg = self.pool_q0 = self.pool_ag = None
             self.pool_sys = self.pool_r = self.pool_stat = self.refill = None

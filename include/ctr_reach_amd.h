@@ -159,7 +159,8 @@ typedef struct ctr_batch_t {
     int32_t  *pool_sys;          /* [P][n]    system index                            */
     uint32_t *pool_r;            /* [P][n]    reset number held (0 = empty)           */
     uint32_t *pool_stat;         /* [P][n]    CTR_STATUS_* of the precomputation      */
-    int32_t  *refill;            /* [1 + 2 refill_cap]: count, then (env, reset number) */
+    int32_t  *refill;            /* [2 + 2 refill_cap]: count, (env, reset number) pairs,
+                                    then a completion ticket (zero-initialised)          */
     int64_t   refill_cap;
 } ctr_batch_t;
 
