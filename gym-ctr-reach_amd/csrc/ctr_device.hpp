@@ -32,10 +32,22 @@ constexpr int RK4_MAX_STEPS = 1 << 20;   // fixed-step RK4: more steps in one se
 // ------------------------------------------------------------------------------------------
 // The 9 gap end points (cumsum(len[0..k]) + min(beta)) live in LDS, one column per lane
 // (s_end[k][lane]: conflict-free, dynamically indexable, off the VGPR budget).
+// Tube presence and curvature per gap are 9-bit masks (bit k = gap k): tube i is present on the
+// gaps [a_i, c_i) and curved on [b_i, c_i) (Segment.py:29-44), so each mask is one range.
 struct Seg {
     uint32_t kept;     // bit k: gap k has non-zero length and ends after s = 0 (kept in S)
-    uint64_t mask;     // 6 bits per gap: bits 0-2 tube i present (EI != 0), 3-5 tube i curved
+    uint64_t pc;       // bits 9i + k: tube i present on gap k; bits 27 + 9i + k: tube i curved
 };
+
+// The 6-bit (present 0-2 | curved 3-5) description of gap k that seg_par takes.
+__device__ __forceinline__ uint32_t seg_bits(const Seg &sg, int k)
+{
+    const uint64_t x = sg.pc >> k;
+    uint32_t b = 0;
+    #pragma unroll
+    for (int j = 0; j < 6; ++j) b |= (uint32_t)((x >> (9 * j)) & 1u) << j;
+    return b;
+}
 
 __device__ __forceinline__ void cswap(double &a, double &b, int &ia, int &ib)
 {
@@ -50,6 +62,11 @@ template <int STRIDE = CTR_BLOCK>      // LDS column stride of end_lds (lanes of
 __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double beta[3], double *end_lds)
 {
 #pragma clang fp contract(off)
+    // per-lane LDS columns: the floored gap lengths and the sorted position of each point, so the
+    // runtime-indexed lookups below are one LDS read instead of a 9-way select chain
+    __shared__ double s_len[9][STRIDE];
+    __shared__ int s_pos[10][STRIDE];
+    const int col = threadIdx.x % STRIDE;
     double v[10];
     int id[10];
     v[0] = 0.0;
@@ -71,39 +88,31 @@ __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double be
     }
     double len[9];
     #pragma unroll
-    for (int k = 0; k < 9; ++k) len[k] = 1e-5 * floor(1e5 * (v[k + 1] - v[k]));   // :16
-
-    uint64_t mask = 0;
+    for (int k = 0; k < 9; ++k) {
+        len[k] = 1e-5 * floor(1e5 * (v[k + 1] - v[k]));   // :16
+        s_len[k][col] = len[k];
+    }
+    #pragma unroll
+    for (int k = 0; k < 10; ++k) s_pos[id[k]][col] = k;   // inverse permutation (argsort positions)
+    // index 9 is never zero-tested by the reference
+    auto len_at = [&](int x) { return x <= 8 ? s_len[x][col] : 1.0; };
+    uint64_t pc = 0;
     #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        int a = 0, b = 0, c = 0;
-        #pragma unroll
-        for (int k = 0; k < 10; ++k) {
-            a = (id[k] == i + 1) ? k : a;
-            b = (id[k] == i + 4) ? k : b;
-            c = (id[k] == i + 7) ? k : c;
-        }
-        auto len_at = [&](int x) {
-            double r = 1.0;              // index 9 is never zero-tested by the reference
-            #pragma unroll
-            for (int k = 0; k < 9; ++k) r = (x == k) ? len[k] : r;
-            return r;
-        };
+        int a = s_pos[i + 1][col], b = s_pos[i + 4][col], c = s_pos[i + 7][col];
         if (len_at(a) == 0) a += 1;       // :29-36
         if (len_at(b) == 0) b += 1;
         if (len_at(a) == 0) a += 1;
         if (c <= 8 && len_at(c) == 0) c += 1;
-        #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            uint64_t pres = (k >= a && k < c) ? 1ull : 0ull;
-            uint64_t curv = (k >= b && k < c) ? 1ull : 0ull;
-            mask |= (pres << (6 * k + i)) | (curv << (6 * k + 3 + i));
-        }
+        const uint32_t upto_c = (1u << c) - 1u;          // gaps < c (c <= 9)
+        const uint32_t pres = upto_c & ~((1u << a) - 1u) & 0x1FFu;
+        const uint32_t curv = upto_c & ~((1u << b) - 1u) & 0x1FFu;
+        pc |= ((uint64_t)pres << (9 * i)) | ((uint64_t)curv << (27 + 9 * i));
     }
     double bmin = fmin(fmin(beta[0], beta[1]), beta[2]);
     Seg sg;
     sg.kept = 0;
-    sg.mask = mask;
+    sg.pc = pc;
     double cum = 0.0;
     #pragma unroll
     for (int k = 0; k < 9; ++k) {         // :46-55 (adding a zero gap is an exact no-op)
@@ -112,14 +121,6 @@ __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double be
         sg.kept |= ((len[k] != 0.0) && (cum + bmin > 0.0)) ? (1u << k) : 0u;
     }
     return sg;
-}
-
-__device__ __forceinline__ double sel9(const double a[9], int k)
-{
-    double r = a[0];
-    #pragma unroll
-    for (int j = 1; j < 9; ++j) r = (k == j) ? a[j] : r;
-    return r;
 }
 
 // A tube system as staged in LDS: the table plus the per-segment divisions precomputed once per
@@ -460,7 +461,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
-            p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), RIGID);
+            p = seg_par(sy, seg_bits(sg, k), RIGID);
             #pragma unroll
             for (int j = 1; j < 3; ++j) {
                 const bool absent = !((p.present >> j) & 1u);
@@ -864,7 +865,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
-            p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), RIGID);
+            p = seg_par(sy, seg_bits(sg, k), RIGID);
             const double endk = end_lds[k * CTR_BLOCK];
             const double a = prev_end, b = endk - 1e-6;
             const double len = fmax(a, b) - fmin(a, b);
@@ -982,7 +983,7 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     bool too_long = false;
     if (rem != 0u) {
         const int k = __builtin_ctz(rem);
-        const SegPar p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), true);
+        const SegPar p = seg_par(sy, seg_bits(sg, k), true);
         const double endk = end_lds[k * CTR_BLOCK];
         const double a = prev_end, b = endk - 1e-6;
         const double len = fmax(a, b) - fmin(a, b);

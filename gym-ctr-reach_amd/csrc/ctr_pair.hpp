@@ -152,7 +152,7 @@ __device__ __forceinline__ void fk_pair_A(const SysK &sy, const double q[6], boo
             } else {
                 const int k = __builtin_ctz(remaining);
                 remaining &= remaining - 1u;
-                p = seg_par(sy, (uint32_t)((sg.mask >> (6 * k)) & 63u), false);
+                p = seg_par(sy, seg_bits(sg, k), false);
                 #pragma unroll
                 for (int j = 1; j < 3; ++j) {
                     const bool absent = !((p.present >> j) & 1u);
