@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ctr_reach_amd.h"
 #include "ctr_math.hpp"
 
@@ -960,6 +962,23 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
 // must call it.  Tips agree with fk_lane_rk4 to rounding (the products associate differently).
 constexpr int SEG_GROUP = 8;
 
+// __shfl_down(x, OFF) inside a 16-lane DPP row (row_shl: lane i reads lane i + OFF of its row):
+// one v_mov_dpp per dword instead of an LDS-crossbar ds_bpermute.  Lanes whose source lies past
+// the row read 0; fk_group_rigid4 uses only lanes whose source is inside their own 8-lane group.
+template <int OFF>
+__device__ __forceinline__ int dpp_down(int x)
+{
+    return __builtin_amdgcn_update_dpp(0, x, 0x100 + OFF, 0xF, 0xF, true);
+}
+
+template <int OFF>
+__device__ __forceinline__ double dpp_down(double x)
+{
+    const long long v = __double_as_longlong(x);
+    const int lo = dpp_down<OFF>((int)(v & 0xffffffffll)), hi = dpp_down<OFF>((int)(v >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 template <bool HAS_UY, bool CAREFUL>
 __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double tip[3], FkStats &st,
                                 double steps_per_m)
@@ -1007,20 +1026,25 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     int any_long = too_long ? 1 : 0;
     #pragma unroll
     for (int off = 1; off < SEG_GROUP; off <<= 1) any_long |= __shfl_xor(any_long, off, SEG_GROUP);
-    // ordered product onto the group's lane 0: round r joins lane j with lane j + 2^r
-    #pragma unroll
-    for (int off = 1; off < SEG_GROUP; off <<= 1) {
+    // ordered product onto the group's lane 0: round r joins lane j with lane j + 2^r (DPP row
+    // shifts: the 8-lane groups sit inside 16-lane rows)
+    static_assert(SEG_GROUP == 8, "the DPP rounds below are written for 8-lane groups");
+    auto join = [&](auto off_tag) {
+        constexpr int off = decltype(off_tag)::value;
         double oq[9], om[3];
         #pragma unroll
-        for (int i = 0; i < 9; ++i) oq[i] = __shfl_down(aq[i], off, SEG_GROUP);
+        for (int i = 0; i < 9; ++i) oq[i] = dpp_down<off>(aq[i]);
         #pragma unroll
-        for (int i = 0; i < 3; ++i) om[i] = __shfl_down(am[i], off, SEG_GROUP);
-        const int on = __shfl_down(nsteps, off, SEG_GROUP);
+        for (int i = 0; i < 3; ++i) om[i] = dpp_down<off>(am[i]);
+        const int on = dpp_down<off>(nsteps);
         if ((j & (2 * off - 1)) == 0) {
             affine_compose(aq, am, oq, om);
             nsteps += on;
         }
-    }
+    };
+    join(std::integral_constant<int, 1>{});
+    join(std::integral_constant<int, 2>{});
+    join(std::integral_constant<int, 4>{});
     // Y = [Rz(alpha_0) | 0] times the product: r = Rz(alpha_0) m  (model.py:57-60)
     double s0, c0;
     ctr_math::sincos_cw(ya[0], &s0, &c0);
@@ -1073,7 +1097,7 @@ __device__ __forceinline__ void obs_lane(const float q[6], const double dg[3], c
         double b = (double)q[i], a = (double)q[3 + i];
         if (egocentric && i > 0) { b -= (double)q[i - 1]; a -= (double)q[3 + i - 1]; }
         double s, c;
-        sincos(a, &s, &c);
+        ctr_math::sincos_cw(a, &s, &c);           // <= 2 ulp (tests/test_math.py), not ocml's sincos
         out[3 * i + 0] = c;
         out[3 * i + 1] = s;
         out[3 * i + 2] = b;
