@@ -41,10 +41,12 @@ FLOP_ATTEMPT = 1050     # stage combinations 15x18 FMA, y_new 5x18, error 6x18, 
 FLOP_SEGMENT = 150      # select_initial_step arithmetic
 FLOP_RK4_STEP = 252     # RK4: 3 stage inputs 3x18 FMA + y_new 18 x 5 (+ stage sums), per step
 FLOP_STEP_EXTRA = 220   # 10 x set_action (160) + reward/obs (60)
-# configs[1] (rigid model, RK4): the executed work of the matrix-power path (csrc/ctr_device.hpp
-# rigid_step_map / affine_compose / fk_group_rigid4), not the stepped RK4 count it replaces
-FLOP_RIGID_MAP = 258    # per segment: [u]x (45) + P, Q, m of the one-step map (three 3x3 products)
-FLOP_COMPOSE = 63       # one 3x4 affine composition (9 x (mul + 2 fma) + 3 x 3 fma)
+# configs[1] (rigid model, RK4): the executed work of the segment-power path (csrc/ctr_device.hpp
+# rigid_segment_map / fk_group_rigid4), not the stepped RK4 count it replaces
+FLOP_RIGID_MAP = 125    # per segment: [u]x (45), the step map's W-polynomial coefficients (23), the
+                        # expansion of M^n to a 3x4 map (57)
+FLOP_COMPOSE = 37       # one composition of two W-polynomial maps (2 x 17 + 3)
+FLOP_TREE = 63          # one general 3x4 affine composition (9 x (mul + 2 fma) + 3 x 3 fma)
 RIGID_TREE = 7          # compositions of the 8-lane group's ordered product (3 shuffle rounds)
 SINCOS_RHS = 3
 PEAK_FP64_VALU = 78.6   # TFLOP/s, MI355X FP64 vector (spec)
@@ -173,7 +175,7 @@ def fk_work(env, joints):
     if env.integrator == "rk4" and env.model == "rigid":
         # k_fk's stats[2] counts the square-and-multiply compositions; k_step's 8-lane groups
         # run the same powers and join the segment maps in RIGID_TREE more compositions
-        per = seg * FLOP_RIGID_MAP + (st["nrej"].double() + RIGID_TREE) * FLOP_COMPOSE
+        per = seg * FLOP_RIGID_MAP + st["nrej"].double() * FLOP_COMPOSE + RIGID_TREE * FLOP_TREE
     elif env.integrator == "rk4":
         per = nfev * FLOP_RHS + att * FLOP_RK4_STEP
     else:
@@ -402,8 +404,9 @@ def main():
                      "hbm_frac_algorithmic": BYTES_STEP * n / (k_ms * 1e-3) / 1e9 / PEAK_HBM,
                      "note": ("bound is the FP64 vector pipe: no GEMM-shaped work for MFMA, far above the HBM ridge; "
                               "peak = MI355X FP64 vector spec; flops from device counters (sincos not priced): " +
-                              ("the EXECUTED work of the rigid matrix-power path (258 flop per segment map + 63 per "
-                               "3x4 composition, incl. the 7 of the 8-lane group product), not the stepped RK4 count"
+                              ("the EXECUTED work of the rigid segment-power path (125 flop per segment map, 37 per "
+                               "W-polynomial composition, 63 per 3x4 composition of the 8-lane group product), not the "
+                               "stepped RK4 count"
                                if cfgd["model"] == "rigid" else "SURVEY 8(d) count"))},
     }
     tr = os.path.join(ROOT, "profiles", "traffic.json")

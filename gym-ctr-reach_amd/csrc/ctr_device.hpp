@@ -360,7 +360,7 @@ __device__ __forceinline__ void shape_put(ShapeOut *so, double s, const double r
 }
 
 // nrej: rejected RK45 attempts; fixed-step RK4 never rejects, so with the rigid model (whose
-// segments run as matrix powers) it counts the 3x4 affine compositions of square-and-multiply.
+// segments run as matrix powers) it counts the map compositions of square-and-multiply.
 struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
@@ -776,41 +776,9 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 // and A = [[W, e3], [0, 0]], W = [u]x.  One classical RK4 step of a linear autonomous ODE is
 // exactly Y <- Y T(hA), T(X) = I + X + X^2/2 + X^3/6 + X^4/24 (its stages collapse to the degree-4
 // Taylor polynomial), i.e. R <- R Q, r <- R m + r with
-//   P = I + (hW/2)(I + (hW/3)(I + hW/4)),  Q = I + hW P,  m = h P e3.
-// The map is built once per segment (3 small matrix products) and the segment's n steps are
-// applied as M^n by square-and-multiply (<= 2 log2 n compositions of 36 FMAs instead of 4n RHS
-// evaluations); results agree with stepping the stages to rounding.
-template <bool HAS_UY>
-__device__ __forceinline__ void rigid_step_map(const SegPar &p, const Trig &t, const double uz[3], double h,
-                                               double Q[9], double m[3])
-{
-    const double I3[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
-    double W[9], dz[3];
-    rhs_core<HAS_UY>(p, t, uz, I3, dz, W);            // I [u]x = W
-    auto mul = [](const double *X, const double *Y, double *Z) {
-        #pragma unroll
-        for (int r = 0; r < 3; ++r)
-            #pragma unroll
-            for (int c = 0; c < 3; ++c)
-                Z[3 * r + c] = fma(X[3 * r + 2], Y[6 + c], fma(X[3 * r + 1], Y[3 + c], X[3 * r] * Y[c]));
-    };
-    double Bm[9], T[9], X[9];
-    #pragma unroll
-    for (int i = 0; i < 9; ++i) Bm[i] = fma(W[i], 0.25 * h, I3[i]);           // I + hW/4
-    #pragma unroll
-    for (int i = 0; i < 9; ++i) X[i] = W[i] * (h * (1.0 / 3.0));
-    mul(X, Bm, T);
-    #pragma unroll
-    for (int i = 0; i < 9; ++i) { T[i] += I3[i]; X[i] = W[i] * (0.5 * h); }    // I + (hW/3)(...)
-    mul(X, T, Bm);
-    #pragma unroll
-    for (int i = 0; i < 9; ++i) { Bm[i] += I3[i]; X[i] = W[i] * h; }           // P
-    mul(X, Bm, Q);
-    #pragma unroll
-    for (int i = 0; i < 9; ++i) Q[i] += I3[i];                                 // Q = I + hW P
-    m[0] = h * Bm[2]; m[1] = h * Bm[5]; m[2] = h * Bm[8];                       // m = h P e3
-}
-
+//   P = I + (hW/2)(I + (hW/3)(I + hW/4)),  Q = I + hW P,  m = h P e3,
+// and the segment's n steps are M^n, computed by square-and-multiply on the coefficients of
+// polynomials in W (rigid_segment_map below); results agree with stepping the stages to rounding.
 // Affine maps applied to row vectors, Y -> Y [[Q, m], [0, 1]]: (Q1, m1) <- (Q1 Q2, Q1 m2 + m1).
 __device__ __forceinline__ void affine_compose(double Q1[9], double m1[3], const double Q2[9], const double m2[3])
 {
@@ -828,14 +796,72 @@ __device__ __forceinline__ void affine_compose(double Q1[9], double m1[3], const
     for (int i = 0; i < 3; ++i) m1[i] = m[i];
 }
 
-__device__ __forceinline__ void affine_square(double Q[9], double m[3])
+// The powers M^n of a segment's one-step map, without 3x3 products.  W = [w]x with w = (u_x0,
+// u_y0, u_z0) satisfies W^3 = -theta^2 W (theta^2 = |w|^2), so every polynomial in W is
+// a I + b W + c W^2: the step map is Q = I + (h - h^3 th^2/6) W + (h^2/2 - h^4 th^2/24) W^2 and
+// m = h P e3 with P = I + (h/2 - h^3 th^2/24) W + (h^2/6) W^2 (the Q and P above with W^3
+// reduced), and composing two maps of the same segment, (Q1 Q2, Q1 m2 + m1), is two products of
+// such triples (10 flop each).  Square-and-multiply on the triples, then one expansion to the
+// 3 x 4 map (W^2 = w w^T - theta^2 I).  Equal to stepping the RK4 stages up to rounding.
+struct WPoly {
+    double a, b, c;    // a I + b W + c W^2
+};
+
+__device__ __forceinline__ WPoly wpoly_mul(const WPoly &x, const WPoly &y, double th2)
 {
-    double Q2[9], m2[3];
+    WPoly r;
+    r.a = x.a * y.a;
+    r.b = fma(x.a, y.b, fma(x.b, y.a, -th2 * fma(x.b, y.c, x.c * y.b)));
+    r.c = fma(x.a, y.c, fma(x.c, y.a, fma(x.b, y.b, -th2 * (x.c * y.c))));
+    return r;
+}
+
+// (Q, m) <- (Q Q2, Q m2 + m) on the triples
+__device__ __forceinline__ void wmap_compose(WPoly &q, WPoly &m, const WPoly &q2, const WPoly &m2, double th2)
+{
+    const WPoly qm = wpoly_mul(q, m2, th2);
+    q = wpoly_mul(q, q2, th2);
+    m.a += qm.a;
+    m.b += qm.b;
+    m.c += qm.c;
+}
+
+// The segment's n RK4 steps of size h (curvature triple w from the segment's constants) as one
+// 3 x 4 map Q [9], m [3].  Returns the number of triple compositions executed.
+template <bool HAS_UY>
+__device__ __forceinline__ int rigid_segment_map(const SegPar &p, const Trig &t, const double uz[3], double h, int n,
+                                                 double Q[9], double m[3])
+{
+    const double I3[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
+    double W[9], dz[3];
+    rhs_core<HAS_UY>(p, t, uz, I3, dz, W);            // I [w]x = W
+    const double wx = W[7], wy = W[2], wz = W[3];
+    const double th2 = fma(wx, wx, fma(wy, wy, wz * wz));
+    const double h2 = h * h, h3 = h2 * h;
+    WPoly sq = {1.0, fma(-h3 * th2, 1.0 / 6.0, h), fma(-h2 * h2 * th2, 1.0 / 24.0, 0.5 * h2)};
+    WPoly sm = {h, h * fma(-h3 * th2, 1.0 / 24.0, 0.5 * h), h * (h2 * (1.0 / 6.0))};
+    WPoly aq = {1.0, 0.0, 0.0}, am = {0.0, 0.0, 0.0};
+    int ncomp = 0;
+    for (int e = n;;) {
+        if (e & 1) { wmap_compose(aq, am, sq, sm, th2); ++ncomp; }   // acc <- acc M^(2^j)
+        e >>= 1;
+        if (!e) break;
+        const WPoly q2 = sq, m2 = sm;
+        wmap_compose(sq, sm, q2, m2, th2);
+        ++ncomp;
+    }
+    const double w[3] = {wx, wy, wz};
+    const double d = fma(-aq.c, th2, aq.a);
     #pragma unroll
-    for (int i = 0; i < 9; ++i) Q2[i] = Q[i];
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) m2[i] = m[i];
-    affine_compose(Q, m, Q2, m2);
+    for (int r = 0; r < 3; ++r)
+        #pragma unroll
+        for (int c = 0; c < 3; ++c)
+            Q[3 * r + c] = fma(aq.c * w[r], w[c], fma(aq.b, W[3 * r + c], r == c ? d : 0.0));
+    // m = am.a e3 + am.b W e3 + am.c (w w_z - theta^2 e3), W e3 = (w_y, -w_x, 0)
+    m[0] = fma(am.b, wy, am.c * (wx * wz));
+    m[1] = fma(-am.b, wx, am.c * (wy * wz));
+    m[2] = fma(am.c, fma(wz, wz, -th2), am.a);
+    return ncomp;
 }
 
 template <bool HAS_UY, bool RIGID, bool CAREFUL = true>
@@ -859,7 +885,6 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
     const Trig tconst = trig_of<CAREFUL>(ya);     // RIGID: the tube angles never change
     SegPar p;
     double h = 0.0, prev_end = 0.0;
-    double rq[9], rm[3];                 // RIGID: the segment's one-step map (rigid_step_map)
     int left = 0;                        // RK4 steps left in the current segment
     uint32_t remaining = sg.kept;
     for (;;) {
@@ -882,18 +907,10 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
             left = (len > 0.0) ? max(1, (int)nf) : 0;
             h = (left > 0) ? len / left : 0.0;
             if (RIGID) {
-                rigid_step_map<HAS_UY>(p, tconst, yu, h, rq, rm);
-                // the segment's `left` steps at once: [R | r] M^left by square-and-multiply
+                // the segment's `left` steps at once: [R | r] M^left (rigid_segment_map)
                 if (left > 0) {
-                    double aq[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, am[3] = {0.0, 0.0, 0.0};
-                    int e = left;
-                    for (;;) {
-                        if (e & 1) { affine_compose(aq, am, rq, rm); st.nrej++; }   // acc <- acc M^(2^j)
-                        e >>= 1;
-                        if (!e) break;
-                        affine_square(rq, rm);
-                        st.nrej++;                  // rigid RK4: nrej counts the compositions
-                    }
+                    double aq[9], am[3];
+                    st.nrej += (uint32_t)rigid_segment_map<HAS_UY>(p, tconst, yu, h, left, aq, am);   // compositions
                     double nR[9];
                     #pragma unroll
                     for (int r = 0; r < 3; ++r) {
@@ -1010,15 +1027,7 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
         too_long = len > 0.0 && !(nf <= (double)RK4_MAX_STEPS);
         const int left = (len > 0.0 && !too_long) ? max(1, (int)nf) : 0;
         if (left > 0) {
-            double rq[9], rm[3];
-            rigid_step_map<HAS_UY>(p, tconst, yu, len / left, rq, rm);
-            int e = left;
-            for (;;) {
-                if (e & 1) affine_compose(aq, am, rq, rm);
-                e >>= 1;
-                if (!e) break;
-                affine_square(rq, rm);
-            }
+            rigid_segment_map<HAS_UY>(p, tconst, yu, len / left, left, aq, am);
             nsteps = left;
         }
     }

@@ -285,7 +285,7 @@ const char *ctr_last_error(void);
 /* Batched Model.forward_kinematics: joints [n][6] f32 -> tip [n][3] f64.
  * sys_idx: [n] or NULL (all system 0).  stats: [n][4] or NULL = {RHS evaluations, accepted
  * RK steps, rejected RK attempts, integrated segments}; fixed-step RK4 never rejects, and with
- * the rigid model stats[2] counts the 3x4 affine compositions of the segments' matrix powers
+ * the rigid model stats[2] counts the map compositions of the segments' matrix powers
  * (the executed work of that path).  status: [n] or NULL.  (device) */
 int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg,
            double *tip, uint32_t *stats, uint32_t *status, void *stream);
