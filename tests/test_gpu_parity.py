@@ -400,6 +400,52 @@ def test_state_dict_roundtrip_replays_exactly(cuda, her_on):
     assert env.sweeps == 0
 
 
+def test_float64_observations_round_to_the_float32_ones(cuda):
+    """obs_dtype="float64" stores the same observation values the float32 env rounds once:
+    two envs on the same seed and actions (auto-resets included) give obs64.float() == obs32
+    and terminal_obs64.float() == terminal_obs32, bit for bit; everything else is identical."""
+    import torch
+    n = 1024
+    kw = dict(seed=31, max_steps_per_episode=4, select_systems=[0, 1, 2, 3])
+    a, b = _env(cuda, n, **kw), _env(cuda, n, obs_dtype="float64", **kw)
+    a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03
+    a.reset(); b.reset()
+    assert b.obs.dtype == torch.float64 and a.obs.dtype == torch.float32
+    assert torch.equal(b.obs.float(), a.obs)
+    rng = np.random.default_rng(5)
+    for _ in range(6):
+        act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * a.action_space.high).astype(np.float32), device=cuda)
+        a.step(act); b.step(act)
+        torch.cuda.synchronize()
+        assert torch.equal(b.obs.float(), a.obs) and torch.equal(b.terminal_obs.float(), a.terminal_obs)
+        for k in ("joints", "achieved_goal", "desired_goal", "t", "epoch", "reward", "done"):
+            assert torch.equal(getattr(a, k), getattr(b, k)), k
+    with pytest.raises(ValueError):
+        b.enable_her()
+
+
+def test_seed_change_rekeys_the_reset_pool(cuda):
+    """seed(s) mid-run re-keys the precomputed resets (ctr_pool_requeue + refill): the pooled
+    auto-resets that follow are the new seed's, identical to an env that pools nothing."""
+    import torch
+    n = 2048
+    kw = dict(max_steps_per_episode=3)
+    a, b = _env(cuda, n, seed=1, pool_depth=0, **kw), _env(cuda, n, seed=1, **kw)
+    for e in (a, b):
+        e.goal_tolerance.current_tol = 1e-12
+        e.reset()
+    z = torch.zeros((n, 6), device=cuda)
+    for e in (a, b):
+        e.step(z)
+        e.seed(77)
+    for _ in range(5):                              # resets at steps 3 and 6 come from seed 77
+        a.step(z); b.step(z)
+    torch.cuda.synchronize()
+    for k in ("joints", "desired_goal", "achieved_goal", "t", "epoch", "obs"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert (b.epoch.cpu().numpy() == 3).all() and b.sweeps == 0
+
+
 @pytest.mark.parametrize("n", [1, 63, 65, 257])
 def test_ragged_batch_sizes_step_vs_oracle(cuda, oracle_mod, n):
     """Batches that are not a multiple of a wave (64) or a workgroup (256): every env's step

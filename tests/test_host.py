@@ -47,6 +47,36 @@ def test_abi_rejects_bad_arguments_without_gpu():
     assert lib.ctr_step(cfg, b, ctypes.c_void_p(1), _abi.CtrStepOut(), 1, None) == -1
 
 
+def test_autoreset_modes_and_pool_requeue_validate_without_gpu():
+    """The round-2 entry points reject bad arguments before any HIP call: an unknown autoreset
+    mode, CTR_AUTORESET_POOLED without a reset pool, a HER store whose t_max / env_base disagree
+    with the config / batch, ctr_pool_requeue without a batch."""
+    from ctr_reach_amd import _abi, systems
+    lib = _abi.load()
+    cfg = systems.make_config(systems.tubes_from_params(systems.default_systems_parameters())[:1])
+    fake = ctypes.c_void_p(16)
+    b = _abi.CtrBatch()
+    b.n = 8
+    b.joints = b.desired_goal = b.achieved_goal = b.t = b.system = b.epoch = b.work = fake
+    o = _abi.CtrStepOut()
+    o.obs = o.reward = o.done = o.success = o.error = fake
+    assert lib.ctr_step(cfg, b, fake, o, 3, None) == -1
+    assert b"autoreset" in lib.ctr_last_error()
+    assert lib.ctr_step(cfg, b, fake, o, _abi.AUTORESET_POOLED, None) == -1
+    assert b"reset pool" in lib.ctr_last_error()
+    h = _abi.CtrHer()
+    h.obs_dim, h.t_max, h.n_sampled_goal, h.strategy, h.n, h.slots = 13, cfg.max_steps + 1, 4, 0, 8, 4
+    h.state = h.step = h.dg = h.tol = h.len = h.epoch = h.cur_t = h.cur_epoch = h.cdf = fake
+    assert lib.ctr_step_her(cfg, b, fake, o, _abi.AUTORESET_SWEEP, h, None) == -1
+    assert b"t_max" in lib.ctr_last_error()
+    h.t_max, h.env_base = cfg.max_steps, 64
+    assert lib.ctr_step_her(cfg, b, fake, o, _abi.AUTORESET_SWEEP, h, None) == -1
+    assert b"env_base" in lib.ctr_last_error()
+    assert lib.ctr_pool_requeue(cfg, None, None) == -1
+    b.n = 0
+    assert lib.ctr_pool_requeue(cfg, b, None) == 0                     # empty batch: no-op
+
+
 def test_struct_layout_matches_header(tmp_path):
     """ctypes mirrors of the ABI structs have the C sizes and every field offset (gcc on the header)."""
     from ctr_reach_amd import _abi
