@@ -10,7 +10,7 @@
 //   fk_lane            envs/model.py:30-70, 119-164 + scipy solve_ivp(RK45) (rk.py, common.py)
 //   set_action_lane    envs/obs.py:166-183
 //   obs_lane           envs/obs.py:136-164, envs/obs_utils.py:41-53,69-80
-//   sample_joints_lane envs/obs.py:185-207 (Philox4x32-10 stream instead of numpy MT19937)
+//   sample_joints_wave envs/obs.py:185-207 (Philox4x32-10 stream instead of numpy MT19937)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -1138,52 +1138,106 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b)
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 
-// Returns the number of candidates drawn; sets q.  Restates obs.py:185-207.  A candidate is six
-// uniforms from three Philox blocks: u0, u1 | u2, u3 | u4, u5; the extensions (u0..u2) decide
-// acceptance, so the third block (the last two angles) is only generated for the accepted
-// candidate -- the same numbers as drawing all three every time, a third fewer blocks per
-// rejected candidate (acceptance is 4-11 %: the slowest lane of a reset wave draws ~40).
-__device__ __forceinline__ int sample_joints_lane(const ctr_system_t &sy, uint64_t seed, uint32_t epoch,
-                                                  uint32_t stream, uint64_t env, float q[6])
+// obs.py:185-207 (sample_goal's rejection sampler) with the build's Philox stream.  A candidate is
+// six uniforms from three Philox blocks 3c, 3c + 1, 3c + 2 (u0, u1 | u2, u3 | u4, u5); the
+// extensions (u0..u2) decide acceptance, so the third block (the last two angles) is generated
+// for the returned candidate only.  Returns the number of candidates drawn (> 1000: the
+// reference's "stuck" case) and sets q.  The wave's lanes help each other (every lane of the wave
+// calls it; `need` marks the lanes that sample).  Lane L's answer is the first accepted candidate of ITS
+// sequence (candidates are keyed by L's env, reset number and stream), so any lane can evaluate
+// any lane's candidate c.  Each round, every lane evaluates one candidate of one unresolved lane:
+// the k unresolved lanes get 64 / k consecutive candidates each, and a lane is resolved by its
+// lowest accepted candidate.  Identical results to sampling each lane alone (candidate 1000 is taken
+// unconditionally, as the serial loop does after 1000 rejections), in ~(sum of tries) / 64 rounds
+// instead of (max tries over the wave).
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int n)
+{
+    // position of the n-th (0-based) set bit of m, by halving the search window
+    int pos = 0;
+    #pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t lo = m & ((w == 64) ? ~0ull : ((1ull << w) - 1ull));
+        const int c = __popcll(lo);
+        if (n >= c) { n -= c; m >>= w; pos += w; }
+        else m = lo;
+    }
+    return pos;
+}
+
+__device__ __forceinline__ int sample_joints_wave(const ctr_system_t &sy, uint64_t seed, uint32_t epoch,
+                                                  uint32_t stream, uint64_t env, bool need, float q[6])
 {
 #pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const uint32_t ctr2 = (uint32_t)env, ctr3 = (uint32_t)(env >> 32) ^ (stream << 24);
-    uint32_t draw = 0;
-    int tries = 0;
+    uint32_t next = 0;               // first candidate of this lane's sequence not yet evaluated
+    uint32_t answer = 0;
+    bool unresolved = need;
     for (;;) {
-        uint32_t c0[4] = {draw, epoch, ctr2, ctr3}, c1[4] = {draw + 1, epoch, ctr2, ctr3};
-        philox(c0, k0, k1);
-        philox(c1, k0, k1);
-        const double u[4] = {u53(c0[0], c0[1]), u53(c0[2], c0[3]), u53(c1[0], c1[1]), u53(c1[2], c1[3])};
-        float b[3];
+        const uint64_t m = __ballot(unresolved);
+        if (!m) break;
+        const int cnt = __popcll(m);
+        const int target = nth_set_bit(m, lane % cnt);
+        const uint32_t c = (uint32_t)__shfl((int)next, target) + (uint32_t)(lane / cnt);
+        const uint32_t t_ep = (uint32_t)__shfl((int)epoch, target);
+        const uint32_t t2 = (uint32_t)__shfl((int)ctr2, target), t3 = (uint32_t)__shfl((int)ctr3, target);
+        double tl[3];
         #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const double lo = (double)(float)(-sy.L[i] + 1e-3);
-            b[i] = (float)(lo + (0.0 - lo) * u[i]);
-        }
-        ++tries;
-        bool ok = true;
-        #pragma unroll
-        for (int i = 1; i < 3; ++i) {
-            const float lhs = b[i - 1] + (float)sy.L[i - 1];
-            const float rhs_ = (float)sy.L[i] + b[i];
-            ok = ok && (b[i - 1] <= b[i]) && (lhs >= rhs_);
-        }
-        if (ok || tries > 1000) {
-            uint32_t c2[4] = {draw + 2, epoch, ctr2, ctr3};
-            philox(c2, k0, k1);
-            const double ua[3] = {u[3], u53(c2[0], c2[1]), u53(c2[2], c2[3])};
+        for (int i = 0; i < 3; ++i) tl[i] = __shfl(sy.L[i], target);
+        bool ok = false;
+        if (c < 1000u) {
+            uint32_t c0[4] = {3u * c, t_ep, t2, t3}, c1[4] = {3u * c + 1u, t_ep, t2, t3};
+            philox(c0, k0, k1);
+            philox(c1, k0, k1);
+            const double u[3] = {u53(c0[0], c0[1]), u53(c0[2], c0[3]), u53(c1[0], c1[1])};
+            float b[3];
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                const double alo = -3.1415927410125732, ahi = 3.1415927410125732;
-                q[i] = b[i];
-                q[3 + i] = (float)(alo + (ahi - alo) * ua[i]);
+                const double lo = (double)(float)(-tl[i] + 1e-3);
+                b[i] = (float)(lo + (0.0 - lo) * u[i]);
             }
-            return tries;
+            ok = true;
+            #pragma unroll
+            for (int i = 1; i < 3; ++i) {
+                const float lhs = b[i - 1] + (float)tl[i - 1];
+                const float rhs_ = (float)tl[i] + b[i];
+                ok = ok && (b[i - 1] <= b[i]) && (lhs >= rhs_);
+            }
+        } else if (c == 1000u) {
+            ok = true;                                    // tries > 1000: the serial loop stops here
         }
-        draw += 3;
+        const uint64_t acc = __ballot(ok);
+        if (unresolved) {
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            uint64_t mine = 0;                            // this lane's helpers: rank, rank + cnt, ...
+            for (int i = rank; i < 64; i += cnt) mine |= 1ull << i;
+            const uint64_t hit = acc & mine;
+            if (hit) {
+                answer = next + (uint32_t)((__builtin_ctzll(hit) - rank) / cnt);
+                unresolved = false;
+            } else {
+                next += (uint32_t)((64 - rank + cnt - 1) / cnt);
+            }
+        }
     }
+    if (!need) return 0;
+    // the chosen candidate in full: extensions and angles (blocks 3a, 3a + 1, 3a + 2)
+    uint32_t c0[4] = {3u * answer, epoch, ctr2, ctr3}, c1[4] = {3u * answer + 1u, epoch, ctr2, ctr3},
+             c2[4] = {3u * answer + 2u, epoch, ctr2, ctr3};
+    philox(c0, k0, k1);
+    philox(c1, k0, k1);
+    philox(c2, k0, k1);
+    const double u[6] = {u53(c0[0], c0[1]), u53(c0[2], c0[3]), u53(c1[0], c1[1]),
+                         u53(c1[2], c1[3]), u53(c2[0], c2[1]), u53(c2[2], c2[3])};
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double lo = (double)(float)(-sy.L[i] + 1e-3);
+        q[i] = (float)(lo + (0.0 - lo) * u[i]);
+        const double alo = -3.1415927410125732, ahi = 3.1415927410125732;
+        q[3 + i] = (float)(alo + (ahi - alo) * u[3 + i]);
+    }
+    return (int)answer + 1;
 }
 
 // Uniform system pick (np.random.randint(n_systems), ctr_reach_env.py:95) from the stream.

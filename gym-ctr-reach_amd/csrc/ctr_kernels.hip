@@ -673,11 +673,11 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
     uint32_t stat = 0;
     float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     double tip[3] = {0.0, 0.0, 0.0};
+    const bool sample = active && (odd ? (kc.c.resample_joints != 0) : (goal == nullptr));
+    // the whole wave samples together (sample_joints_wave): every lane calls it
+    if (sample_joints_wave(sy, seed, r, odd ? 1u : 0u, genv, sample, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
     if (active) {
-        const bool sample = odd ? (kc.c.resample_joints != 0) : (goal == nullptr);
-        if (sample) {
-            if (sample_joints_lane(sy, seed, r, odd ? 1u : 0u, genv, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
-        } else if (odd) {
+        if (!sample && odd) {
             #pragma unroll
             for (int k = 0; k < 6; ++k) qv[k] = q_cur[k];
         }
