@@ -36,6 +36,10 @@ constexpr int RK4_MAX_STEPS = 1 << 20;   // fixed-step RK4: more steps in one se
 // (s_end[k][lane]: conflict-free, dynamically indexable, off the VGPR budget).
 // Tube presence and curvature per gap are 9-bit masks (bit k = gap k): tube i is present on the
 // gaps [a_i, c_i) and curved on [b_i, c_i) (Segment.py:29-44), so each mask is one range.
+// One column per lane of a 256-lane workgroup, shared by every FK variant a kernel instantiates
+// (a function-scope __shared__ array would be allocated once per template instantiation).
+__shared__ double s_seg_end[9][CTR_BLOCK];
+
 struct Seg {
     uint32_t kept;     // bit k: gap k has non-zero length and ends after s = 0 (kept in S)
     uint64_t pc;       // bits 9i + k: tube i present on gap k; bits 27 + 9i + k: tube i curved
@@ -64,10 +68,9 @@ template <int STRIDE = CTR_BLOCK>      // LDS column stride of end_lds (lanes of
 __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double beta[3], double *end_lds)
 {
 #pragma clang fp contract(off)
-    // per-lane LDS columns: the floored gap lengths and the sorted position of each point, so the
-    // runtime-indexed lookups below are one LDS read instead of a 9-way select chain
-    __shared__ double s_len[9][STRIDE];
-    __shared__ int s_pos[10][STRIDE];
+    // per-lane LDS column: the sorted position of each point (argsort), so the runtime-indexed
+    // lookups below are one LDS read instead of a 10-way select chain; zero-length gaps as a mask
+    __shared__ uint8_t s_pos[10][STRIDE];
     const int col = threadIdx.x % STRIDE;
     double v[10];
     int id[10];
@@ -89,23 +92,24 @@ __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double be
         for (int i = (r & 1); i + 1 < 10; i += 2) cswap(v[i], v[i + 1], id[i], id[i + 1]);
     }
     double len[9];
+    uint32_t zero = 0;                    // bit k: gap k floored to zero length
     #pragma unroll
     for (int k = 0; k < 9; ++k) {
         len[k] = 1e-5 * floor(1e5 * (v[k + 1] - v[k]));   // :16
-        s_len[k][col] = len[k];
+        zero |= (len[k] == 0.0) ? (1u << k) : 0u;
     }
     #pragma unroll
-    for (int k = 0; k < 10; ++k) s_pos[id[k]][col] = k;   // inverse permutation (argsort positions)
-    // index 9 is never zero-tested by the reference
-    auto len_at = [&](int x) { return x <= 8 ? s_len[x][col] : 1.0; };
+    for (int k = 0; k < 10; ++k) s_pos[id[k]][col] = (uint8_t)k;   // inverse permutation (argsort positions)
+    // len_at(x) == 0 (index 9 is never zero-tested by the reference)
+    auto zero_at = [&](int x) { return ((zero >> x) & 1u) != 0u; };
     uint64_t pc = 0;
     #pragma unroll
     for (int i = 0; i < 3; ++i) {
         int a = s_pos[i + 1][col], b = s_pos[i + 4][col], c = s_pos[i + 7][col];
-        if (len_at(a) == 0) a += 1;       // :29-36
-        if (len_at(b) == 0) b += 1;
-        if (len_at(a) == 0) a += 1;
-        if (c <= 8 && len_at(c) == 0) c += 1;
+        if (zero_at(a)) a += 1;           // :29-36
+        if (zero_at(b)) b += 1;
+        if (zero_at(a)) a += 1;
+        if (c <= 8 && zero_at(c)) c += 1;
         const uint32_t upto_c = (1u << c) - 1u;          // gaps < c (c <= 9)
         const uint32_t pres = upto_c & ~((1u << a) - 1u) & 0x1FFu;
         const uint32_t curv = upto_c & ~((1u << b) - 1u) & 0x1FFu;
@@ -131,6 +135,8 @@ __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double be
 struct SysK : ctr_system_t {
     double kz[3];
     double inv[8];
+    const double *lut;   // [64][8]: seg_par of every 6-bit gap description (wx, g, inv, present),
+                         // staged per workgroup by stage_systems, or nullptr (per-lane tables)
 };
 
 __device__ __forceinline__ void sysk_derive(SysK &s, int j)
@@ -170,6 +176,24 @@ __device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool r
     for (int j = 0; j < 3; ++j) p.g[j] = (p.kz[j] * p.ux0[j]) * p.inv;
     p.present = (uint32_t)(bits6 & 7u);
     return p;
+}
+
+// seg_par from the workgroup's table when the RHS needs only (wx, g, inv, present): no y
+// pre-curvature, compliant model, a shared system row (per-lane tables have lut == nullptr).
+// Four LDS reads instead of the per-tube selects and products at every segment start.
+template <bool HAS_UY, bool RIGID>
+__device__ __forceinline__ SegPar seg_par_at(const SysK &sy, uint32_t bits6)
+{
+    if (!HAS_UY && !RIGID && sy.lut) {
+        SegPar p = {};
+        const double *e = sy.lut + 8 * bits6;
+        #pragma unroll
+        for (int j = 0; j < 3; ++j) { p.wx[j] = e[j]; p.g[j] = e[3 + j]; }
+        p.inv = e[6];
+        p.present = (uint32_t)e[7];
+        return p;
+    }
+    return seg_par(sy, bits6, RIGID);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -414,8 +438,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 {
     using namespace rk;
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};
-    __shared__ double s_end[9][CTR_BLOCK];
-    double *end_lds = &s_end[0][threadIdx.x];
+    double *end_lds = &s_seg_end[0][threadIdx.x];
     const Seg sg = seg_build(sy, beta, end_lds);
 
     // state y = [u_z(3), alpha(3), r(3), R(9)]
@@ -463,7 +486,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
-            p = seg_par(sy, seg_bits(sg, k), RIGID);
+            p = seg_par_at<HAS_UY, RIGID>(sy, seg_bits(sg, k));
             #pragma unroll
             for (int j = 1; j < 3; ++j) {
                 const bool absent = !((p.present >> j) & 1u);
@@ -868,8 +891,7 @@ template <bool HAS_UY, bool RIGID, bool CAREFUL = true>
 __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], FkStats &st, double steps_per_m)
 {
     const double beta[3] = {q[0], q[1], q[2]};
-    __shared__ double s_end4[9][CTR_BLOCK];
-    double *end_lds = &s_end4[0][threadIdx.x];
+    double *end_lds = &s_seg_end[0][threadIdx.x];
     const Seg sg = seg_build(sy, beta, end_lds);
     double yu[3] = {0.0, 0.0, 0.0};
     double ya[3] = {q[3], q[4], q[5]};
@@ -892,7 +914,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
-            p = seg_par(sy, seg_bits(sg, k), RIGID);
+            p = seg_par_at<HAS_UY, RIGID>(sy, seg_bits(sg, k));
             const double endk = end_lds[k * CTR_BLOCK];
             const double a = prev_end, b = endk - 1e-6;
             const double len = fmax(a, b) - fmin(a, b);
@@ -1001,8 +1023,7 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
                                 double steps_per_m)
 {
     const double beta[3] = {q[0], q[1], q[2]};
-    __shared__ double s_endg[9][CTR_BLOCK];
-    double *end_lds = &s_endg[0][threadIdx.x];
+    double *end_lds = &s_seg_end[0][threadIdx.x];
     const Seg sg = seg_build(sy, beta, end_lds);
     const double ya[3] = {q[3], q[4], q[5]};
     const double yu[3] = {0.0, 0.0, 0.0};

@@ -80,6 +80,17 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tub
     __syncthreads();
     for (int i = threadIdx.x; i < kc.c.n_systems * 11; i += blockDim.x) sysk_derive(lds[i / 11], i % 11);
     __syncthreads();
+    // seg_par of every (system, 6-bit gap description): SysK::lut, read at segment starts
+    __shared__ double s_lut[CTR_MAX_SYSTEMS][64][8];
+    for (int i = threadIdx.x; i < kc.c.n_systems * 64; i += blockDim.x) {
+        const SegPar q = seg_par(lds[i / 64], (uint32_t)(i % 64), false);
+        double *e = s_lut[i / 64][i % 64];
+        for (int j = 0; j < 3; ++j) { e[j] = q.wx[j]; e[3 + j] = q.g[j]; }
+        e[6] = q.inv;
+        e[7] = (double)q.present;
+    }
+    for (int i = threadIdx.x; i < kc.c.n_systems; i += blockDim.x) lds[i].lut = &s_lut[i][0][0];
+    __syncthreads();
 }
 
 __device__ __forceinline__ int clamp_sys(int s, int n) { return (s < 0 || s >= n) ? 0 : s; }
@@ -104,6 +115,7 @@ __device__ __forceinline__ const SysK &episode_sys(const KCfg &kc, const SysK *s
     domain_system(s_sys[s], s_raw[s], kc.c.domain_rand, kc.c.seed, epoch, genv, me, nullptr);
     #pragma unroll
     for (int j = 0; j < 11; ++j) sysk_derive(me, j);
+    me.lut = nullptr;
     return me;
 }
 
@@ -312,6 +324,7 @@ __global__ __launch_bounds__(BLOCK) void k_fk_shape(KCfg kc, const float *__rest
             static_cast<ctr_system_t &>(me) = tables[e];
             #pragma unroll
             for (int j = 0; j < 11; ++j) sysk_derive(me, j);
+            me.lut = nullptr;
             sy = &me;
         }
         FkStats st = {0, 0, 0, 0, 0};
