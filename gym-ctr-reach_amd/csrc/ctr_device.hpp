@@ -178,6 +178,17 @@ __device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool r
     return p;
 }
 
+// No y pre-curvature: the RHS uses inv only as a factor of every wx product, so fold it in
+// (wx <- inv wx, and g = kz ux0 inv becomes kz ux0): two fewer products per RHS.
+__device__ __forceinline__ void seg_fold_inv(SegPar &p)
+{
+    #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        p.wx[j] = p.wx[j] * p.inv;
+        p.g[j] = p.kz[j] * p.ux0[j];
+    }
+}
+
 // seg_par from the workgroup's table when the RHS needs only (wx, g, inv, present): no y
 // pre-curvature, compliant model, a shared system row (per-lane tables have lut == nullptr).
 // Four LDS reads instead of the per-tube selects and products at every segment start.
@@ -193,7 +204,9 @@ __device__ __forceinline__ SegPar seg_par_at(const SysK &sy, uint32_t bits6)
         p.present = (uint32_t)e[7];
         return p;
     }
-    return seg_par(sy, bits6, RIGID);
+    SegPar p = seg_par(sy, bits6, RIGID);
+    if (!HAS_UY) seg_fold_inv(p);
+    return p;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -210,13 +223,13 @@ struct Trig {
 };
 
 #ifndef CTR_TRIG_POLY
-// (sin, cos)(k pi/64) table for sincos_tab, one copy per workgroup in LDS; every kernel that
+// (sin, cos)(k pi/256) table for sincos_tab, one copy per workgroup in LDS; every kernel that
 // integrates calls trig_table_fill() before its first barrier.
-__shared__ double s_trig_tab[128][2];
+__shared__ double s_trig_tab[512][2];
 
 __device__ __forceinline__ void trig_table_fill()
 {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
 }
 #else
 __device__ __forceinline__ void trig_table_fill() {}
@@ -282,8 +295,8 @@ __device__ __forceinline__ void rhs_core(const SegPar &p, const Trig &t, const d
         duz[0] = -(p.g[0] * sy1);
         duz[1] = -(p.g[1] * sy2);
         duz[2] = p.g[2] * sy3;
-        const double a = p.inv * fma(p.wx[2], t.c20, fma(p.wx[1], t.c10, p.wx[0]));   // ux_0
-        const double b = p.inv * sy1;                                                  // uy_0
+        const double a = fma(p.wx[2], t.c20, fma(p.wx[1], t.c10, p.wx[0]));   // ux_0 (wx = inv EI Ux)
+        const double b = sy1;                                                 // uy_0
         const double u0 = uz[0];
         #pragma unroll
         for (int r = 0; r < 3; ++r) {                             // dR = R [u]x  (model.py:103-110)
@@ -1040,7 +1053,8 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     bool too_long = false;
     if (rem != 0u) {
         const int k = __builtin_ctz(rem);
-        const SegPar p = seg_par(sy, seg_bits(sg, k), true);
+        SegPar p = seg_par(sy, seg_bits(sg, k), true);
+        if (!HAS_UY) seg_fold_inv(p);
         const double endk = end_lds[k * CTR_BLOCK];
         const double a = prev_end, b = endk - 1e-6;
         const double len = fmax(a, b) - fmin(a, b);

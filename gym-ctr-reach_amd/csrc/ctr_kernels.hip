@@ -83,7 +83,8 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tub
     // seg_par of every (system, 6-bit gap description): SysK::lut, read at segment starts
     __shared__ double s_lut[CTR_MAX_SYSTEMS][64][8];
     for (int i = threadIdx.x; i < kc.c.n_systems * 64; i += blockDim.x) {
-        const SegPar q = seg_par(lds[i / 64], (uint32_t)(i % 64), false);
+        SegPar q = seg_par(lds[i / 64], (uint32_t)(i % 64), false);
+        seg_fold_inv(q);
         double *e = s_lut[i / 64][i % 64];
         for (int j = 0; j < 3; ++j) { e[j] = q.wx[j]; e[3 + j] = q.g[j]; }
         e[6] = q.inv;

@@ -80,168 +80,58 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
 
 CTR_HD bool sincos_needs_slow(double x) { return !(fabs(x) < 1048576.0); }
 
-// Table-based sincos: x = n (pi/64) + r, |r| <= pi/128, with (sin, cos)(k pi/64), k = n mod 128,
-// from a 2 KB table (kept in LDS by the kernels) and short Taylor kernels on r:
+// Table-based sincos: x = n (pi/256) + r, |r| <= pi/512, with (sin, cos)(k pi/256), k = n mod 512,
+// from an 8 KB table (kept in LDS by the kernels) and short Taylor kernels on r:
 //   sin x = S_k cos r + C_k sin r,   cos x = C_k cos r - S_k sin r.
-// Degree 7 / 6 kernels (truncation < 4e-18 on |r| <= 0.0246) and a two-term Cody-Waite reduction
-// (the third pi/64 term is below 1e-28 for |x| < 2^20): 16 fp64 operations per angle, no
-// quadrant selects.  One wave per SIMD makes the FK loop issue-bound, so every operation counts.
-// Max error <= 2 ulp (tests/test_math.py).  Valid for |x| < 2^20 like sincos_fast.
-constexpr double TRIG_TAB[128][2] = {
-    {0x0.0p+0, 0x1.0000000000000p+0},
-    {0x1.91f65f10dd814p-5, 0x1.ff621e3796d7ep-1},
-    {0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
-    {0x1.2c8106e8e613ap-3, 0x1.fa7557f08a517p-1},
-    {0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1},
-    {0x1.f19f97b215f1bp-3, 0x1.f0a7efb9230d7p-1},
-    {0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1},
-    {0x1.58f9a75ab1fddp-2, 0x1.e212104f686e5p-1},
-    {0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1},
-    {0x1.b5d1009e15cc0p-2, 0x1.ced7af43cc773p-1},
-    {0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1},
-    {0x1.073879922ffeep-1, 0x1.b728345196e3ep-1},
-    {0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1},
-    {0x1.30ff7fce17035p-1, 0x1.9b3e047f38741p-1},
-    {0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1},
-    {0x1.57d69348ceca0p-1, 0x1.7b5df226aafafp-1},
-    {0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1},
-    {0x1.7b5df226aafafp-1, 0x1.57d69348ceca0p-1},
-    {0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1},
-    {0x1.9b3e047f38741p-1, 0x1.30ff7fce17035p-1},
-    {0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1},
-    {0x1.b728345196e3ep-1, 0x1.073879922ffeep-1},
-    {0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2},
-    {0x1.ced7af43cc773p-1, 0x1.b5d1009e15cc0p-2},
-    {0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2},
-    {0x1.e212104f686e5p-1, 0x1.58f9a75ab1fddp-2},
-    {0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
-    {0x1.f0a7efb9230d7p-1, 0x1.f19f97b215f1bp-3},
-    {0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3},
-    {0x1.fa7557f08a517p-1, 0x1.2c8106e8e613ap-3},
-    {0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4},
-    {0x1.ff621e3796d7ep-1, 0x1.91f65f10dd814p-5},
-    {0x1.0000000000000p+0, 0x1.77d4c76273645p-204},
-    {0x1.ff621e3796d7ep-1, -0x1.91f65f10dd814p-5},
-    {0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4},
-    {0x1.fa7557f08a517p-1, -0x1.2c8106e8e613ap-3},
-    {0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3},
-    {0x1.f0a7efb9230d7p-1, -0x1.f19f97b215f1bp-3},
-    {0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2},
-    {0x1.e212104f686e5p-1, -0x1.58f9a75ab1fddp-2},
-    {0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2},
-    {0x1.ced7af43cc773p-1, -0x1.b5d1009e15cc0p-2},
-    {0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2},
-    {0x1.b728345196e3ep-1, -0x1.073879922ffeep-1},
-    {0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1},
-    {0x1.9b3e047f38741p-1, -0x1.30ff7fce17035p-1},
-    {0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1},
-    {0x1.7b5df226aafafp-1, -0x1.57d69348ceca0p-1},
-    {0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1},
-    {0x1.57d69348ceca0p-1, -0x1.7b5df226aafafp-1},
-    {0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1},
-    {0x1.30ff7fce17035p-1, -0x1.9b3e047f38741p-1},
-    {0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1},
-    {0x1.073879922ffeep-1, -0x1.b728345196e3ep-1},
-    {0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1},
-    {0x1.b5d1009e15cc0p-2, -0x1.ced7af43cc773p-1},
-    {0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1},
-    {0x1.58f9a75ab1fddp-2, -0x1.e212104f686e5p-1},
-    {0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1},
-    {0x1.f19f97b215f1bp-3, -0x1.f0a7efb9230d7p-1},
-    {0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1},
-    {0x1.2c8106e8e613ap-3, -0x1.fa7557f08a517p-1},
-    {0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1},
-    {0x1.91f65f10dd814p-5, -0x1.ff621e3796d7ep-1},
-    {0x1.77d4c76273645p-203, -0x1.0000000000000p+0},
-    {-0x1.91f65f10dd814p-5, -0x1.ff621e3796d7ep-1},
-    {-0x1.917a6bc29b42cp-4, -0x1.fd88da3d12526p-1},
-    {-0x1.2c8106e8e613ap-3, -0x1.fa7557f08a517p-1},
-    {-0x1.8f8b83c69a60bp-3, -0x1.f6297cff75cb0p-1},
-    {-0x1.f19f97b215f1bp-3, -0x1.f0a7efb9230d7p-1},
-    {-0x1.294062ed59f06p-2, -0x1.e9f4156c62ddap-1},
-    {-0x1.58f9a75ab1fddp-2, -0x1.e212104f686e5p-1},
-    {-0x1.87de2a6aea963p-2, -0x1.d906bcf328d46p-1},
-    {-0x1.b5d1009e15cc0p-2, -0x1.ced7af43cc773p-1},
-    {-0x1.e2b5d3806f63bp-2, -0x1.c38b2f180bdb1p-1},
-    {-0x1.073879922ffeep-1, -0x1.b728345196e3ep-1},
-    {-0x1.1c73b39ae68c8p-1, -0x1.a9b66290ea1a3p-1},
-    {-0x1.30ff7fce17035p-1, -0x1.9b3e047f38741p-1},
-    {-0x1.44cf325091dd6p-1, -0x1.8bc806b151741p-1},
-    {-0x1.57d69348ceca0p-1, -0x1.7b5df226aafafp-1},
-    {-0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bcdp-1},
-    {-0x1.7b5df226aafafp-1, -0x1.57d69348ceca0p-1},
-    {-0x1.8bc806b151741p-1, -0x1.44cf325091dd6p-1},
-    {-0x1.9b3e047f38741p-1, -0x1.30ff7fce17035p-1},
-    {-0x1.a9b66290ea1a3p-1, -0x1.1c73b39ae68c8p-1},
-    {-0x1.b728345196e3ep-1, -0x1.073879922ffeep-1},
-    {-0x1.c38b2f180bdb1p-1, -0x1.e2b5d3806f63bp-2},
-    {-0x1.ced7af43cc773p-1, -0x1.b5d1009e15cc0p-2},
-    {-0x1.d906bcf328d46p-1, -0x1.87de2a6aea963p-2},
-    {-0x1.e212104f686e5p-1, -0x1.58f9a75ab1fddp-2},
-    {-0x1.e9f4156c62ddap-1, -0x1.294062ed59f06p-2},
-    {-0x1.f0a7efb9230d7p-1, -0x1.f19f97b215f1bp-3},
-    {-0x1.f6297cff75cb0p-1, -0x1.8f8b83c69a60bp-3},
-    {-0x1.fa7557f08a517p-1, -0x1.2c8106e8e613ap-3},
-    {-0x1.fd88da3d12526p-1, -0x1.917a6bc29b42cp-4},
-    {-0x1.ff621e3796d7ep-1, -0x1.91f65f10dd814p-5},
-    {-0x1.0000000000000p+0, 0x1.dcc40d4ec52eap-199},
-    {-0x1.ff621e3796d7ep-1, 0x1.91f65f10dd814p-5},
-    {-0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4},
-    {-0x1.fa7557f08a517p-1, 0x1.2c8106e8e613ap-3},
-    {-0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3},
-    {-0x1.f0a7efb9230d7p-1, 0x1.f19f97b215f1bp-3},
-    {-0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
-    {-0x1.e212104f686e5p-1, 0x1.58f9a75ab1fddp-2},
-    {-0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2},
-    {-0x1.ced7af43cc773p-1, 0x1.b5d1009e15cc0p-2},
-    {-0x1.c38b2f180bdb1p-1, 0x1.e2b5d3806f63bp-2},
-    {-0x1.b728345196e3ep-1, 0x1.073879922ffeep-1},
-    {-0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c8p-1},
-    {-0x1.9b3e047f38741p-1, 0x1.30ff7fce17035p-1},
-    {-0x1.8bc806b151741p-1, 0x1.44cf325091dd6p-1},
-    {-0x1.7b5df226aafafp-1, 0x1.57d69348ceca0p-1},
-    {-0x1.6a09e667f3bcdp-1, 0x1.6a09e667f3bcdp-1},
-    {-0x1.57d69348ceca0p-1, 0x1.7b5df226aafafp-1},
-    {-0x1.44cf325091dd6p-1, 0x1.8bc806b151741p-1},
-    {-0x1.30ff7fce17035p-1, 0x1.9b3e047f38741p-1},
-    {-0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a3p-1},
-    {-0x1.073879922ffeep-1, 0x1.b728345196e3ep-1},
-    {-0x1.e2b5d3806f63bp-2, 0x1.c38b2f180bdb1p-1},
-    {-0x1.b5d1009e15cc0p-2, 0x1.ced7af43cc773p-1},
-    {-0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1},
-    {-0x1.58f9a75ab1fddp-2, 0x1.e212104f686e5p-1},
-    {-0x1.294062ed59f06p-2, 0x1.e9f4156c62ddap-1},
-    {-0x1.f19f97b215f1bp-3, 0x1.f0a7efb9230d7p-1},
-    {-0x1.8f8b83c69a60bp-3, 0x1.f6297cff75cb0p-1},
-    {-0x1.2c8106e8e613ap-3, 0x1.fa7557f08a517p-1},
-    {-0x1.917a6bc29b42cp-4, 0x1.fd88da3d12526p-1},
-    {-0x1.91f65f10dd814p-5, 0x1.ff621e3796d7ep-1},
+// Degree 5 / 4 kernels (truncation < 7e-20 relative for sin, < 7.4e-17 absolute for cos) and a
+// two-term Cody-Waite reduction (the third pi/256 term is below 1e-28 for |x| < 2^20): 14 fp64
+// operations per angle, no quadrant selects.  One wave per SIMD makes the FK loop issue-bound,
+// so every operation counts (the pi/64 table with degree-7 / 6 kernels took 16).  Max error
+// <= 2 ulp (tests/test_math.py).  Valid for |x| < 2^20 like sincos_fast.
+#include "ctr_trig_tab512.inc"
+
+// Split in two so callers can issue the reduction and the table loads a stage ahead of the
+// polynomial work that consumes them (one wave per SIMD cannot hide the LDS latency otherwise).
+struct TabPre {
+    double r0, r1;               // reduced arguments, |r| <= pi/512
+    double ts0, tc0, ts1, tc1;   // (sin, cos)(k pi/256) of each angle
 };
 
-// Two angles at once: both reductions and both table loads are issued before either pair of
-// Taylor kernels, so the LDS latency of the table reads hides behind the polynomial work.
+CTR_HD TabPre sincos_tab2_pre(double x0, double x1, const double (*tab)[2])
+{
+    TabPre p;
+    const double n0 = rint(x0 * 81.48733086305042), n1 = rint(x1 * 81.48733086305042);   // round(x 256/pi)
+    const int k0 = ((int)n0) & 511, k1 = ((int)n1) & 511;
+    p.ts0 = tab[k0][0];
+    p.tc0 = tab[k0][1];
+    p.ts1 = tab[k1][0];
+    p.tc1 = tab[k1][1];
+    p.r0 = fma(-n0, 4.783776559169348e-19, fma(-n0, 0.01227184630308513, x0));
+    p.r1 = fma(-n1, 4.783776559169348e-19, fma(-n1, 0.01227184630308513, x1));
+    return p;
+}
+
+CTR_HD void sincos_tab2_post(const TabPre &p, double &s0, double &c0, double &s1, double &c1)
+{
+    const double r0 = p.r0, r1 = p.r1;
+    const double z0 = r0 * r0, z1 = r1 * r1;
+    // sin r = r + r z (-1/6 + z / 120),  cos r = 1 + z (-1/2 + z / 24)
+    const double sp0 = fma(z0, 8.3333333333333332e-03, -1.6666666666666666e-01);
+    const double sp1 = fma(z1, 8.3333333333333332e-03, -1.6666666666666666e-01);
+    const double cp0 = fma(z0, 4.1666666666666664e-02, -0.5);
+    const double cp1 = fma(z1, 4.1666666666666664e-02, -0.5);
+    const double sr0 = fma(r0 * z0, sp0, r0), sr1 = fma(r1 * z1, sp1, r1);
+    const double cr0 = fma(z0, cp0, 1.0), cr1 = fma(z1, cp1, 1.0);
+    s0 = fma(p.ts0, cr0, p.tc0 * sr0);
+    c0 = fma(p.tc0, cr0, -(p.ts0 * sr0));
+    s1 = fma(p.ts1, cr1, p.tc1 * sr1);
+    c1 = fma(p.tc1, cr1, -(p.ts1 * sr1));
+}
+
 CTR_HD void sincos_tab2(double x0, double x1, const double (*tab)[2], double &s0, double &c0, double &s1,
                         double &c1)
 {
-    const double n0 = rint(x0 * 20.371832715762604), n1 = rint(x1 * 20.371832715762604);   // round(x 64/pi)
-    const int k0 = ((int)n0) & 127, k1 = ((int)n1) & 127;
-    const double ts0 = tab[k0][0], tc0 = tab[k0][1];
-    const double ts1 = tab[k1][0], tc1 = tab[k1][1];
-    double r0 = fma(-n0, 0.04908738521234052, x0), r1 = fma(-n1, 0.04908738521234052, x1);
-    r0 = fma(-n0, 1.9135106236677394e-18, r0);
-    r1 = fma(-n1, 1.9135106236677394e-18, r1);
-    const double z0 = r0 * r0, z1 = r1 * r1;
-    // sin r = r + r z (-1/6 + z (1/120 - z / 5040)),  cos r = 1 + z (-1/2 + z (1/24 - z / 720))
-    const double sp0 = fma(z0, fma(z0, -1.9841269841269841e-04, 8.3333333333333332e-03), -1.6666666666666666e-01);
-    const double sp1 = fma(z1, fma(z1, -1.9841269841269841e-04, 8.3333333333333332e-03), -1.6666666666666666e-01);
-    const double cp0 = fma(z0, fma(z0, -1.3888888888888889e-03, 4.1666666666666664e-02), -0.5);
-    const double cp1 = fma(z1, fma(z1, -1.3888888888888889e-03, 4.1666666666666664e-02), -0.5);
-    const double sr0 = fma(r0 * z0, sp0, r0), sr1 = fma(r1 * z1, sp1, r1);
-    const double cr0 = fma(z0, cp0, 1.0), cr1 = fma(z1, cp1, 1.0);
-    s0 = fma(ts0, cr0, tc0 * sr0);
-    c0 = fma(tc0, cr0, -(ts0 * sr0));
-    s1 = fma(ts1, cr1, tc1 * sr1);
-    c1 = fma(tc1, cr1, -(ts1 * sr1));
+    sincos_tab2_post(sincos_tab2_pre(x0, x1, tab), s0, c0, s1, c1);
 }
 
 CTR_HD void sincos_tab(double x, const double (*tab)[2], double &sv, double &cv)
@@ -249,6 +139,7 @@ CTR_HD void sincos_tab(double x, const double (*tab)[2], double &sv, double &cv)
     double s1, c1;
     sincos_tab2(x, 0.0, tab, sv, cv, s1, c1);
 }
+
 
 CTR_HD void sincos_cw(double x, double *sp, double *cp)
 {

@@ -15,7 +15,8 @@ def _lib(tmp_path):
                    'extern "C" void vsincos(const double* x, double* s, double* c, long n) {\n'
                    '  for (long i = 0; i < n; ++i) ctr_math::sincos_cw(x[i], s + i, c + i); }\n'
                    'extern "C" void vsincos_tab(const double* x, double* s, double* c, long n) {\n'
-                   '  for (long i = 0; i < n; ++i) ctr_math::sincos_tab(x[i], ctr_math::TRIG_TAB, s[i], c[i]); }\n')
+                   '  for (long i = 0; i < n; ++i) ctr_math::sincos_tab(x[i], ctr_math::TRIG_TAB, s[i], c[i]); }\n'
+                   )
     so = tmp_path / "m.so"
     subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-shared", "-fPIC",
                            "-I", os.path.join(ROOT, "gym-ctr-reach_amd", "csrc"), str(src), "-o", str(so)])
@@ -39,7 +40,8 @@ def test_sincos_accuracy(tmp_path, fn):
     x = np.concatenate([rng.uniform(-np.pi, np.pi, 200000), rng.uniform(-300, 300, 200000),
                         rng.uniform(-1e5, 1e5, 50000), np.array([0.0, -0.0, 1e-300, np.pi / 2, -np.pi]),
                         np.arange(-40, 41) * (np.pi / 2), np.arange(-40, 41) * (np.pi / 2) + 1e-9,
-                        np.arange(-400, 401) * (np.pi / 32), np.arange(-400, 401) * (np.pi / 32) + 1e-12])
+                        np.arange(-400, 401) * (np.pi / 32), np.arange(-400, 401) * (np.pi / 32) + 1e-12,
+                        np.arange(-1600, 1601) * (np.pi / 256), np.arange(-1600, 1601) * (np.pi / 512)])
     if fn == "vsincos":          # sincos_cw has the exact large-argument path; sincos_tab is |x| < 2^20
         x = np.concatenate([x, [1e6, 3e7]])
     s = np.empty_like(x)
