@@ -84,6 +84,10 @@ def parse():
     ap.add_argument("--systems", default="0",
                     help="select_systems, comma-separated registration indices (default 0, the headline; "
                          "'0,1,2,3' is SURVEY.md 8(d)'s mixed-system divergence check)")
+    ap.add_argument("--untimed-min", type=int, default=480,
+                    help="at least this many untimed steps before the window, and at least one episode "
+                         "length + --warmup (the clocks of a GPU that just started stepping settle over "
+                         "the first ~30-50 ms of sustained load)")
     return ap.parse_args()
 
 
@@ -305,11 +309,18 @@ def main():
         if gather:
             _, works[k] = env.gather_outputs(async_op=True)
 
-    # untimed: one whole episode length (every env passes a time-limit reset), then the warmup
-    for i in range(max_steps + args.warmup):
+    # the window's bookkeeping (and the first barrier) once here: their first use loads kernels /
+    # builds communicators for tens of ms, and a GPU left idle that long before the window drops
+    # its clocks (the first steps after such a gap ran 94-102 us instead of 88-90 us)
+    env.epoch.to(torch.int64).sum().item()
+    if dist:
+        dist.barrier()
+    # untimed: one whole episode length (every env passes a time-limit reset) and the warmup,
+    # rounded up to whole refill periods so the last untimed step ends with a pool refill and the
+    # window starts on a refill boundary with the GPU still busy
+    pre = -(-max(max_steps + args.warmup, args.untimed_min) // R) * R
+    for i in range(pre):
         one_step(i)
-    env.refill_pool()                # the window starts on a refill boundary
-    torch.cuda.synchronize()
     if args.profile_only:
         for i in range(args.steps):
             one_step(i)
@@ -351,6 +362,8 @@ def main():
     k_iters = max(5, min(args.steps, 32))
     sp = _abi.stream_ptr(stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for i in range(64):              # untimed: back to sustained-load clocks after fk_work's host sync
+        _abi.check(env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[i % len(acts)]), env._out, 0, sp), "ctr_step")
     e0.record(stream)
     for i in range(k_iters):
         rc = env.lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[i % len(acts)]), env._out, 0, sp)
@@ -389,7 +402,7 @@ def main():
                    "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,
                                   "autoreset": "pooled (no miss sweep)" if env.pool_depth >= env.refill_interval
                                   else "pooled + miss sweep"},
-                   "steady_state": {"staggered_t": not args.no_stagger, "untimed_steps_before": max_steps + args.warmup,
+                   "steady_state": {"staggered_t": not args.no_stagger, "untimed_steps_before": pre,
                                     "resets_in_window": resets, "refills_in_window": refills * ws,
                                     "refills_in_window_per_rank": refills,
                                     "miss_sweep_launches_in_window_per_rank": sweeps,
