@@ -27,6 +27,7 @@ time measured with HIP events on the launch stream) and the CPU oracle timed on 
 (cpu_baseline, rank 0 only).
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -328,6 +329,9 @@ def main():
         return 0
 
     # ---- timed region: K whole-job steps, auto-resets and pool refills at their natural rate
+    # (a host pause while the first launches are queued starves the GPU: no collector pass inside)
+    gc.collect()
+    gc.disable()
     epoch0 = env.epoch.to(torch.int64).sum()
     refills0, sweeps0 = env.refills, env.sweeps
     if dist:
@@ -342,6 +346,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    gc.enable()
     el = D.max_over_ranks(time.perf_counter() - t0, device=dev if backend in (None, "nccl") else "cpu")
     resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
     refills = env.refills - refills0
