@@ -7,6 +7,7 @@ Attempt counts per segment come from the CPU oracle on env-trajectory joints.  P
   now        I whenever any lane needs it, then A in the same iteration (fk_lane today)
   batch K W  I only when >= K lanes wait for it, or a lane has waited W iterations, or no lane
              has an attempt to run; waiting lanes idle through the attempt block
+`python tools/sim_sched.py sort` compares wave regroupings by predicted work instead.
 """
 import os
 import sys
@@ -80,7 +81,34 @@ def simulate(att, policy, K=1, W=0, CI=0.43, CA=1.0):
     return total / (n / 64), iters_tot / (n / 64)
 
 
+def sort_study(n=16384, seed=3):
+    """Wave regrouping by predicted work (the previous step's attempt counts): the launch is as
+    long as its slowest wave (one wave per SIMD, all resident at once), so compare max, not mean."""
+    q = trajectory_joints(n, 10, seed=seed)
+    rng = np.random.default_rng(seed + 2)
+    hi = np.array([0.001, 0.001, 0.001, np.deg2rad(5), np.deg2rad(5), np.deg2rad(5)], np.float32)
+    a = ((rng.random((n, 6)) * 2 - 1) * hi).astype(np.float32)
+    att_prev = oracle.fk_segattempts(q)
+    att = oracle.fk_segattempts(oracle.step(q, a, np.zeros((n, 3)), np.zeros(n, np.int32), 0.02)["joints"])
+
+    def waves(x):
+        return np.array([simulate(x[w:w + 64], "now")[0] for w in range(0, len(x), 64)])
+
+    key = att_prev.sum(1) * 16 + (att_prev > 0).sum(1)
+    orders = {"natural": np.arange(n), "global, previous step": np.argsort(key, kind="stable"),
+              "global, this step": np.argsort(att.sum(1) * 16 + (att > 0).sum(1), kind="stable")}
+    for b in (256, 1024):
+        orders["blocks of %d, previous step" % b] = np.concatenate(
+            [b0 + np.argsort(key[b0:b0 + b], kind="stable") for b0 in range(0, n, b)])
+    for name, o in orders.items():
+        c = waves(att[o])
+        print("%-28s wave cost mean %.2f  p99 %.2f  max %.2f" % (name, c.mean(), np.quantile(c, 0.99), c.max()))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "sort":
+        sort_study()
+        sys.exit(0)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     q = trajectory_joints(n, 12)
     att = oracle.fk_segattempts(q)
