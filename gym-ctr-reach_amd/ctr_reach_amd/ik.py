@@ -15,8 +15,12 @@ reference's solver loops forever there) stops at its last finite iterate with er
 """
 
 
-def dls_ik_position_only(env, targets, q0, system=None, lam=0.25, num=500, tol=1e-3, eps=1e-4):
-    """targets [M, 3], q0 [M, 6] (float64 tensors or arrays) -> (q [M, 6], err [M], iters [M])."""
+def dls_ik_position_only(env, targets, q0, system=None, lam=0.25, num=500, tol=1e-3, eps=1e-4, check_every=8):
+    """targets [M, 3], q0 [M, 6] (float64 tensors or arrays) -> (q [M, 6], err [M], iters [M]).
+
+    The iteration is stream-ordered: every iteration runs on the whole batch with finished targets
+    masked out, and the host reads the "any target still active" flag only every
+    ``check_every`` iterations (to stop early), so the loop does not synchronise per iteration."""
     import torch
     dev = env.device
     pd = torch.as_tensor(targets, dtype=torch.float64, device=dev).reshape(-1, 3)
@@ -27,28 +31,24 @@ def dls_ik_position_only(env, targets, q0, system=None, lam=0.25, num=500, tol=1
     err = torch.full((m,), float("inf"), dtype=torch.float64, device=dev)
     iters = torch.zeros(m, dtype=torch.int32, device=dev)
     eye = lam * torch.eye(3, dtype=torch.float64, device=dev)
-    for _ in range(int(num)):
-        idx = torch.nonzero(active).flatten()
-        if idx.numel() == 0:
+    nan = torch.tensor(float("nan"), dtype=torch.float64, device=dev)
+    for k in range(int(num)):
+        if k % max(1, int(check_every)) == 0 and not bool(active.any()):
             break
-        s = None if sys_t is None else sys_t[idx]
-        p, jac = env.jacobian(q[idx], s, eps=eps)
-        e = pd[idx] - p
-        bad = ~torch.isfinite(e).all(dim=1) | ~torch.isfinite(jac).flatten(1).all(dim=1)
-        if bool(bad.any()):
-            # the iterate left the nesting constraints into a tube gap (NaN FK, where the
-            # reference's solver never returns): stop that target at its last finite iterate
-            err[idx[bad]] = float("nan")
-            active[idx[bad]] = False
-            keep = ~bad
-            idx, p, jac, e = idx[keep], p[keep], jac[keep], e[keep]
-            if idx.numel() == 0:
-                continue
-        jjt = jac @ jac.transpose(1, 2) + eye
-        dq = (jac.transpose(1, 2) @ torch.linalg.solve(jjt, e.unsqueeze(-1))).squeeze(-1)
-        q[idx] += dq
-        en = torch.linalg.norm(e, dim=1)
-        err[idx] = en
-        iters[idx] += 1
-        active[idx] = en >= tol
+        p, jac = env.jacobian(q, sys_t, eps=eps)
+        e = pd - p
+        # an iterate that left the nesting constraints into a tube gap (NaN FK, where the
+        # reference's solver never returns) stops at its last finite iterate with err = NaN
+        bad = active & (~torch.isfinite(e).all(dim=1) | ~torch.isfinite(jac).flatten(1).all(dim=1))
+        err = torch.where(bad, nan, err)
+        live = active & ~bad
+        jl = torch.where(live[:, None, None], jac, torch.zeros_like(jac))
+        el = torch.where(live[:, None], e, torch.zeros_like(e))
+        jjt = jl @ jl.transpose(1, 2) + eye
+        dq = (jl.transpose(1, 2) @ torch.linalg.solve(jjt, el.unsqueeze(-1))).squeeze(-1)
+        q = torch.where(live[:, None], q + dq, q)
+        en = torch.linalg.norm(el, dim=1)
+        err = torch.where(live, en, err)
+        iters = iters + live.to(torch.int32)
+        active = live & (en >= tol)
     return q, err, iters
