@@ -320,6 +320,10 @@ def main():
     # rounded up to whole refill periods so the last untimed step ends with a pool refill and the
     # window starts on a refill boundary with the GPU still busy
     pre = -(-max(max_steps + args.warmup, args.untimed_min) // R) * R
+    # no collector pass from here to the end of the window: a full pass takes tens of ms (a host
+    # pause that idles the GPU before the window, or starves it while the window is queued)
+    gc.collect()
+    gc.disable()
     for i in range(pre):
         one_step(i)
     if args.profile_only:
@@ -329,9 +333,6 @@ def main():
         return 0
 
     # ---- timed region: K whole-job steps, auto-resets and pool refills at their natural rate
-    # (a host pause while the first launches are queued starves the GPU: no collector pass inside)
-    gc.collect()
-    gc.disable()
     epoch0 = env.epoch.to(torch.int64).sum()
     refills0, sweeps0 = env.refills, env.sweeps
     if dist:

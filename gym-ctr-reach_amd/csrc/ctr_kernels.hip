@@ -406,6 +406,39 @@ __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict
 
 // The per-env tail of CtrReachEnv.step after the FK (ctr_reach_env.py:136-158): reward, done,
 // success, error, observation, and the auto-reset from the pool (or the miss flag).
+// The pooled reset of an env whose episode hits the time limit this step (t + 1 >= max_steps:
+// done whatever the FK gives, ~86 % of the resets at steady state), loaded when the step starts.
+// The reset path at the end of the step then needs no dependent HBM round trips (pool_r, then
+// the row) on the slowest wave's critical path; the other resets still load theirs at the end.
+struct PoolPre {
+    bool loaded = false;
+    uint32_t pr;            // pool_r of the slot (the reset number it holds)
+    int32_t sys;
+    uint32_t stat;
+    float q0[6], qd[6];
+    double dg[3], ag[3];
+};
+
+__device__ __forceinline__ void pool_prefetch(const KCfg &kc, const ctr_batch_t &b, int64_t e, int32_t autoreset,
+                                              PoolPre &pp)
+{
+    const int P = b.pool_depth;
+    if (!autoreset || P <= 0 || b.t[e] + 1 < kc.c.max_steps) return;
+    const uint32_t r = b.epoch[e] + 1;
+    const int64_t ps = (int64_t)(r % (uint32_t)P) * b.n + e;
+    pp.loaded = true;
+    pp.pr = b.pool_r[ps];
+    pp.sys = b.pool_sys[ps];
+    pp.stat = b.pool_stat[ps];
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) pp.q0[i] = b.pool_q0[6 * ps + i];
+    if (b.desired_joints)
+        #pragma unroll
+        for (int i = 0; i < 6; ++i) pp.qd[i] = b.pool_qd[6 * ps + i];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { pp.dg[i] = b.pool_dg[3 * ps + i]; pp.ag[i] = b.pool_ag[3 * ps + i]; }
+}
+
 struct StepFlags {
     bool miss = false;       // done, but no pooled reset available -> k_reset
     bool pooled = false;     // done and reset from the pool -> queue the refill
@@ -414,7 +447,8 @@ struct StepFlags {
 
 __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o, int64_t e,
                                             int s, float q[6], double ag[3], const FkStats &st, int32_t autoreset,
-                                            StepFlags &fl, const ctr_her_t *her, const float *action)
+                                            StepFlags &fl, const ctr_her_t *her, const float *action,
+                                            const PoolPre &pp)
 {
     const int32_t t = b.t[e] + 1;
     double dg[3];
@@ -458,16 +492,19 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
         const uint32_t r = b.epoch[e] + 1;                      // reset number to take
         const int P = b.pool_depth;
         const int64_t ps = P > 0 ? (int64_t)(r % (uint32_t)P) * b.n + e : 0;
-        if (P > 0 && b.pool_r[ps] == r) {
+        if (P > 0 && (pp.loaded ? pp.pr : b.pool_r[ps]) == r) {
             // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
-            const int s2 = clamp_sys(b.pool_sys[ps], kc.c.n_systems);
+            const int s2 = clamp_sys(pp.loaded ? pp.sys : b.pool_sys[ps], kc.c.n_systems);
             #pragma unroll
-            for (int i = 0; i < 6; ++i) q[i] = b.pool_q0[6 * ps + i];
+            for (int i = 0; i < 6; ++i) q[i] = pp.loaded ? pp.q0[i] : b.pool_q0[6 * ps + i];
             #pragma unroll
-            for (int i = 0; i < 3; ++i) { dg[i] = b.pool_dg[3 * ps + i]; ag[i] = b.pool_ag[3 * ps + i]; }
+            for (int i = 0; i < 3; ++i) {
+                dg[i] = pp.loaded ? pp.dg[i] : b.pool_dg[3 * ps + i];
+                ag[i] = pp.loaded ? pp.ag[i] : b.pool_ag[3 * ps + i];
+            }
             if (b.desired_joints)
                 #pragma unroll
-                for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = b.pool_qd[6 * ps + i];
+                for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = pp.loaded ? pp.qd[i] : b.pool_qd[6 * ps + i];
             if (b.starting_joints)
                 #pragma unroll
                 for (int i = 0; i < 6; ++i) b.starting_joints[6 * e + i] = q[i];
@@ -478,7 +515,7 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
             for (int i = 0; i < 3; ++i) b.desired_goal[3 * e + i] = dg[i];
             b.system[e] = s2;
             b.epoch[e] = r;
-            stat |= b.pool_stat[ps];
+            stat |= pp.loaded ? pp.stat : b.pool_stat[ps];
             obs_lane(q, dg, ag, kc.c.tol, s2, multi, kc.c.egocentric != 0, obs);
             if (her) {                                              // the next episode starts now
                 float obf[14];
@@ -536,6 +573,8 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
             for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(s_sys[s], kc.c.constrain_alpha != 0, q, a);
         }
+        PoolPre pp;
+        if (live) pool_prefetch(kc, b, e, autoreset, pp);
         const SysK &sy = in ? episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)) : s_sys[0];
         const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
         FkStats st = {0, 0, 0, 0, 0};
@@ -544,13 +583,15 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             fk_group_rigid4<(MODE & 1) != 0, true>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
         else
             fk_group_rigid4<(MODE & 1) != 0, false>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
-        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e);
+        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
     } else if (live) {
         const int s = clamp_sys(b.system[e], kc.c.n_systems);
         const SysK &sy = s_sys[s];
         float q[6], a[6];
         #pragma unroll
         for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
+        PoolPre pp;
+        pool_prefetch(kc, b, e, autoreset, pp);
         for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(sy, kc.c.constrain_alpha != 0, q, a);
         FkStats st = {0, 0, 0, 0, 0};
         double ag[3];
@@ -559,7 +600,7 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
 #else
         fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);
 #endif
-        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e);
+        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
     }
     if (autoreset) {
         if (autoreset == CTR_AUTORESET_POOLED) {
@@ -627,7 +668,7 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
         double ag[3];
         if (fk_needs_careful_trig(qd)) fk_pair_A<(MODE & 1) != 0, true>(sy, qd, live, ag, st, X);
         else fk_pair_A<(MODE & 1) != 0, false>(sy, qd, live, ag, st, X);
-        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e);
+        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, PoolPre{});
     } else {
         fk_pair_B(X);
     }
