@@ -450,6 +450,9 @@ template <bool HAS_UY, bool RIGID, bool SHAPE = false, bool CAREFUL = true>
 __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st, ShapeOut *so = nullptr)
 {
     using namespace rk;
+    // f's alpha part is the masked u_z of y (stage_at, and K6 -> f on acceptance): it is read
+    // from y instead of being carried in f (three fewer loop-carried doubles)
+#define CTR_FAL(i) ((i) == 0 ? (((p.present & 1u) != 0u) ? yu[0] : 0.0) : yu[i])
     const double beta[3] = {(double)q[0], (double)q[1], (double)q[2]};
     double *end_lds = &s_seg_end[0][threadIdx.x];
     const Seg sg = seg_build(sy, beta, end_lds);
@@ -558,7 +561,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             for (int i = 0; i < 3; ++i) {
                 s0 += (yuref[i] * isc_u[i]) * (yuref[i] * isc_u[i]) + (ya[i] * isc_a[i]) * (ya[i] * isc_a[i]) +
                       (yr[i] * isc_r[i]) * (yr[i] * isc_r[i]);
-                s1 += (f.uz[i] * isc_u[i]) * (f.uz[i] * isc_u[i]) + (f.al[i] * isc_a[i]) * (f.al[i] * isc_a[i]) +
+                s1 += (f.uz[i] * isc_u[i]) * (f.uz[i] * isc_u[i]) + (CTR_FAL(i) * isc_a[i]) * (CTR_FAL(i) * isc_a[i]) +
                       (fr[i] * isc_r[i]) * (fr[i] * isc_r[i]);
             }
             #pragma unroll
@@ -574,7 +577,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             h0 = fmin(h0, interval);
             double u1[3], a1[3], R1[9];
             #pragma unroll
-            for (int i = 0; i < 3; ++i) { u1[i] = yu[i] + h0 * f.uz[i]; a1[i] = ya[i] + h0 * f.al[i]; }
+            for (int i = 0; i < 3; ++i) { u1[i] = yu[i] + h0 * f.uz[i]; a1[i] = ya[i] + h0 * CTR_FAL(i); }
             #pragma unroll
             for (int i = 0; i < 9; ++i) R1[i] = yR[i] + h0 * f.R[i];
             Stage f1;
@@ -588,7 +591,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             double s2 = 0.0;
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                const double du = (f1.uz[i] - f.uz[i]) * isc_u[i], da = (f1.al[i] - f.al[i]) * isc_a[i],
+                const double du = (f1.uz[i] - f.uz[i]) * isc_u[i], da = (f1.al[i] - CTR_FAL(i)) * isc_a[i],
                              dr = (f1r[i] - fr[i]) * isc_r[i];
                 s2 += du * du + da * da + dr * dr;
             }
@@ -681,15 +684,15 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
                 _Pragma("unroll") for (int i = 0; i < 3; ++i)                                  \
                     _Pragma("unroll") for (int j = 0; j < 4; ++j) qr[i][j] += rc[i] * PROW[j]; \
         }
-        CTR_STAGE(K1, c1(f.uz[i], yu[i]), c1(f.al[i], ya[i]), c1(f.R[i], yR[i]), 0.0, 0.0, P1)
-        CTR_STAGE(K2, c2(f.uz[i], K1.uz[i], yu[i]), c2(f.al[i], K1.al[i], ya[i]), c2(f.R[i], K1.R[i], yR[i]),
+        CTR_STAGE(K1, c1(f.uz[i], yu[i]), c1(CTR_FAL(i), ya[i]), c1(f.R[i], yR[i]), 0.0, 0.0, P1)
+        CTR_STAGE(K2, c2(f.uz[i], K1.uz[i], yu[i]), c2(CTR_FAL(i), K1.al[i], ya[i]), c2(f.R[i], K1.R[i], yR[i]),
                   B2, E2, P2)
-        CTR_STAGE(K3, c3(f.uz[i], K1.uz[i], K2.uz[i], yu[i]), c3(f.al[i], K1.al[i], K2.al[i], ya[i]),
+        CTR_STAGE(K3, c3(f.uz[i], K1.uz[i], K2.uz[i], yu[i]), c3(CTR_FAL(i), K1.al[i], K2.al[i], ya[i]),
                   c3(f.R[i], K1.R[i], K2.R[i], yR[i]), B3, E3, P3)
-        CTR_STAGE(K4, c4(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], yu[i]), c4(f.al[i], K1.al[i], K2.al[i], K3.al[i], ya[i]),
+        CTR_STAGE(K4, c4(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], yu[i]), c4(CTR_FAL(i), K1.al[i], K2.al[i], K3.al[i], ya[i]),
                   c4(f.R[i], K1.R[i], K2.R[i], K3.R[i], yR[i]), B4, E4, P4)
         CTR_STAGE(K5, c5(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], K4.uz[i], yu[i]),
-                  c5(f.al[i], K1.al[i], K2.al[i], K3.al[i], K4.al[i], ya[i]),
+                  c5(CTR_FAL(i), K1.al[i], K2.al[i], K3.al[i], K4.al[i], ya[i]),
                   c5(f.R[i], K1.R[i], K2.R[i], K3.R[i], K4.R[i], yR[i]), B5, E5, P5)
 #undef CTR_STAGE
         CTR_STAMP(ts2);
@@ -703,10 +706,10 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
             nu[i] = cb(f.uz[i], K2.uz[i], K3.uz[i], K4.uz[i], K5.uz[i], yu[i]);
-            na[i] = cb(f.al[i], K2.al[i], K3.al[i], K4.al[i], K5.al[i], ya[i]);
+            na[i] = cb(CTR_FAL(i), K2.al[i], K3.al[i], K4.al[i], K5.al[i], ya[i]);
             nr[i] = yr[i] + h * br[i];
             eu[i] = f.uz[i] * E0 + K2.uz[i] * E2 + K3.uz[i] * E3 + K4.uz[i] * E4 + K5.uz[i] * E5;
-            ea[i] = f.al[i] * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5;
+            ea[i] = CTR_FAL(i) * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5;
         }
         #pragma unroll
         for (int i = 0; i < 9; ++i) {
@@ -799,6 +802,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 #endif
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+#undef CTR_FAL
 }
 
 // ------------------------------------------------------------------------------------------

@@ -872,7 +872,12 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         const int64_t e = active ? b.refill[1 + 2 * i] : 0;
         const uint32_t r = active ? (uint32_t)b.refill[2 + 2 * i] : 0;
         const int64_t ps = active ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
-        const bool fresh = active && b.pool_r[ps] != r;
+        // only the resets the env can still take from its ring, epoch + 1 .. epoch + P.  With a
+        // ring shallower than the refill interval one period can queue both r + P (the env took
+        // reset r from the ring) and r + 2P (the miss sweep took r + P when the ring ran dry):
+        // the two map to one slot, and writing both would race (fields of two resets mixed)
+        const uint32_t ep = active ? (uint32_t)b.epoch[e] : 0u;
+        const bool fresh = active && b.pool_r[ps] != r && r - ep - 1u < (uint32_t)b.pool_depth;
         const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
                                                nullptr, -1);
         if (fresh && odd) {

@@ -299,13 +299,51 @@ def test_facade_gym_surface(cuda):
         env.close()
 
 
+def test_refill_writes_only_resets_the_env_can_take(cuda):
+    """k_refill writes a queued (env, r) only when epoch < r <= epoch + P: two queued resets for
+    one ring slot (r and r + P) can then never both be written (they would race)."""
+    import torch
+    env = _env(cuda, 256, seed=3, pool_depth=2, refill_interval=1000)
+    env.reset()
+    torch.cuda.synchronize()
+    e = 7
+    ep = int(env.epoch[e].item())
+    slot = (ep + 1) % 2
+    assert int(env.pool_r[slot, e].item()) == ep + 1          # reset() filled the ring
+    row = {k: getattr(env, k)[slot, e].clone() for k in ("pool_q0", "pool_qd", "pool_dg", "pool_ag", "pool_sys")}
+    env.pool_r[slot, e] = 0                                    # the slot looks empty
+    # queue a reset the env has already taken (same slot: ep - 1), then the one it needs next
+    q = env.refill
+    q.zero_()
+    q[0] = 2
+    q[1], q[2] = e, ep - 1
+    q[3], q[4] = e, ep + 1
+    env.refill_pool()
+    torch.cuda.synchronize()
+    assert int(env.pool_r[slot, e].item()) == ep + 1
+    for k, v in row.items():
+        assert torch.equal(getattr(env, k)[slot, e], v), k     # the row of reset ep + 1, not a mix
+    # only the stale entry queued: the slot is left alone
+    env.pool_r[slot, e] = 0
+    q.zero_()
+    q[0] = 1
+    q[1], q[2] = e, ep - 1
+    env.refill_pool()
+    torch.cuda.synchronize()
+    assert int(env.pool_r[slot, e].item()) == 0
+    assert int(env.refill[0].item()) == 0                      # the refill cleared its queue
+
+
 @pytest.mark.parametrize("depth,interval,rand", [(4, 8, 0.0), (1, 1000, 0.0), (2, 3, 0.0), (4, 8, 0.05),
-                                                  (8, 4, 0.0), (5, 5, 0.05)])
+                                                  (8, 4, 0.0), (5, 5, 0.05), (1, 4, 0.0), (2, 7, 0.0)])
 def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
     """Pooled auto-resets (precomputed ahead of time, consumed by a copy; including pool misses
     that fall back to the synchronous path) give bit-identical trajectories to computing every
     reset at the step that needs it: a reset is a pure function of (seed, env id, reset number).
-    depth >= interval: every step runs CTR_AUTORESET_POOLED (no miss sweep launched at all)."""
+    depth >= interval: every step runs CTR_AUTORESET_POOLED (no miss sweep launched at all).
+    depth < interval: one refill period queues several resets for the same ring slot (taken from
+    the ring, then swept after the ring ran dry); the refill writes only the ones the env can
+    still take (an intermittent mixed-slot race before that rule)."""
     import torch
     n = 4096
     kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3], domain_rand=rand)
