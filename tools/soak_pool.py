@@ -1,0 +1,37 @@
+"""Soak check of the reset pool (GPU): 150 steps of 8 192 envs with a reset roughly every other
+step, pooled auto-resets (several ring depths / refill intervals, domain randomisation) against
+synchronous resets, every state array compared bit for bit every 10 steps.  A longer cousin of
+tests/test_gpu_parity.py::test_reset_pool_matches_synchronous_resets for rare races."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gym-ctr-reach_amd"))
+from ctr_reach_amd import CtrReachVecEnv  # noqa: E402
+cuda = torch.device("cuda", 0)
+n = 8192
+configs = [(0, 1, 0.0), (2, 3, 0.0), (1, 4, 0.05), (3, 7, 0.0), (5, 5, 0.05), (8, 4, 0.0)]
+bad = 0
+for depth, interval, rand in configs:
+    kw = dict(seed=5 + depth, max_steps_per_episode=5, select_systems=[0, 1, 2, 3], domain_rand=rand)
+    a = CtrReachVecEnv(n, device=cuda, pool_depth=0, **kw)
+    b = CtrReachVecEnv(n, device=cuda, pool_depth=depth, refill_interval=interval, **kw) if depth else \
+        CtrReachVecEnv(n, device=cuda, pool_depth=8, refill_interval=3, **kw)
+    a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.04
+    a.reset(); b.reset()
+    rng = np.random.default_rng(depth * 7 + interval)
+    for step in range(150):
+        act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * a.action_space.high).astype(np.float32), device=cuda)
+        a.step(act); b.step(act)
+        if step % 10 == 9:
+            torch.cuda.synchronize()
+            for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs"):
+                if not torch.equal(getattr(a, k), getattr(b, k)):
+                    bad += 1
+                    print("MISMATCH", depth, interval, rand, step, k, flush=True)
+                    break
+    print("config", depth, interval, rand, "resets", int(a.epoch.sum().item()), "ok" if bad == 0 else "bad", flush=True)
+print("TOTAL BAD", bad)
+sys.exit(1 if bad else 0)

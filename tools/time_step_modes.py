@@ -1,5 +1,6 @@
 """Diagnostic: k_step time (HIP events, 100 back-to-back launches after 300 warm ones) for the
-library named by CTR_REACH_AMD_LIB, with auto-reset off and with the pooled auto-reset."""
+library named by CTR_REACH_AMD_LIB, with auto-reset off and with the pooled auto-reset.
+usage: python tools/time_step_modes.py [n_envs] [rigid]"""
 import os
 import sys
 
@@ -10,7 +11,10 @@ sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
 from ctr_reach_amd import CtrReachVecEnv, _abi  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-env = CtrReachVecEnv(n, device="cuda", seed=0, refill_interval=64)
+kw = {}
+if len(sys.argv) > 2 and sys.argv[2] == "rigid":      # configs[1]: rigid model, RK4 at 100 steps/m
+    kw = dict(integrator="rk4", rk4_steps_per_m=100, model="rigid")
+env = CtrReachVecEnv(n, device="cuda", seed=0, refill_interval=64, **kw)
 env.reset()
 g = torch.Generator(device="cuda")
 g.manual_seed(1)
