@@ -864,9 +864,17 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     __shared__ int64_t s_count;
     if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
     stage_systems(kc, s_sys, s_raw);
-    const int64_t per_grid = (int64_t)gridDim.x * (BLOCK / 2);
-    for (int64_t base = (int64_t)blockIdx.x * (BLOCK / 2); base < s_count; base += per_grid) {
-        const int64_t i = base + (threadIdx.x >> 1);
+    // entries are dealt round-robin over the waves of the first (at most) 256 workgroups, one
+    // wave per SIMD of the chip: a typical refill (~10 k entries) then puts ~10 resets on every
+    // wave instead of 32 on a third of them, and a wave lasts as long as its slowest lane
+    const int64_t G = min((int64_t)gridDim.x, (int64_t)256);
+    const int64_t waves = G * (BLOCK / 64);
+    const int64_t per_pass = waves * 32;                  // 32 lane pairs per wave
+    const int64_t my_wave = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const int64_t my_pair = (threadIdx.x & 63) >> 1;
+    const int64_t count = blockIdx.x < G ? s_count : 0;
+    for (int64_t base = 0; base < count; base += per_pass) {
+        const int64_t i = base + my_pair * waves + my_wave;
         const bool odd = threadIdx.x & 1;
         const bool active = i < s_count;
         const int64_t e = active ? b.refill[1 + 2 * i] : 0;

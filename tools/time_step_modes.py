@@ -20,7 +20,9 @@ g = torch.Generator(device="cuda")
 g.manual_seed(1)
 hi = torch.tensor(env.action_space.high, device="cuda")
 acts = [((torch.rand((n, 6), generator=g, device="cuda") * 2 - 1) * hi).contiguous() for _ in range(8)]
-env.t.copy_(torch.randint(0, 150, (n,), dtype=torch.int32, device="cuda"))
+g0 = torch.Generator(device="cpu")
+g0.manual_seed(2)
+env.t.copy_(torch.randint(0, 150, (n,), generator=g0, dtype=torch.int32))
 stream = torch.cuda.current_stream()
 sp = _abi.stream_ptr(stream)
 for mode, name in ((0, "autoreset off"), (_abi.AUTORESET_POOLED, "pooled auto-reset")):
