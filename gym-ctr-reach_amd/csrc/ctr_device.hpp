@@ -1136,19 +1136,42 @@ __device__ __forceinline__ void set_action_lane(const ctr_system_t &sy, bool con
 }
 
 // obs.py:136-164.  Writes obs_dim (13 or 14) values in float64, the reference's dtype; the env
-// stores them as float32 (rounded once) or float64 (ctr_env_config_t.obs_f64).
+// stores them as float32 (rounded once) or float64 (ctr_env_config_t.obs_f64).  Needs the
+// workgroup's trig table (trig_table_fill, done by stage_systems).
 __device__ __forceinline__ void obs_lane(const float q[6], const double dg[3], const double ag[3], double tol,
                                          int sys, bool multi, bool egocentric, double *out)
 {
+    double b[3], a[3], s[3], c[3];
     #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        double b = (double)q[i], a = (double)q[3 + i];
-        if (egocentric && i > 0) { b -= (double)q[i - 1]; a -= (double)q[3 + i - 1]; }
-        double s, c;
-        ctr_math::sincos_cw(a, &s, &c);           // <= 2 ulp (tests/test_math.py), not ocml's sincos
-        out[3 * i + 0] = c;
-        out[3 * i + 1] = s;
-        out[3 * i + 2] = b;
+        b[i] = (double)q[i];
+        a[i] = (double)q[3 + i];
+        if (egocentric && i > 0) { b[i] -= (double)q[i - 1]; a[i] -= (double)q[3 + i - 1]; }
+    }
+    // the workgroup's LDS sincos table (<= 2 ulp, tests/test_math.py, like sincos_cw); angles
+    // beyond its |x| < 2^20 range (never reached by bounded episodes) take the exact path
+#ifndef CTR_TRIG_POLY
+    ctr_math::sincos_tab2(a[0], a[1], s_trig_tab, s[0], c[0], s[1], c[1]);
+    ctr_math::sincos_tab(a[2], s_trig_tab, s[2], c[2]);
+#else
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) ctr_math::sincos_fast(a[i], s[i], c[i]);
+#endif
+    if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(a[0]) || ctr_math::sincos_needs_slow(a[1]) ||
+                                  ctr_math::sincos_needs_slow(a[2])) != 0, 0)) {
+        #pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (ctr_math::sincos_needs_slow(a[i])) {
+                const ctr_math::SinCos r = ctr_math::sincos_slow(a[i]);
+                s[i] = r.s;
+                c[i] = r.c;
+            }
+    }
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        out[3 * i + 0] = c[i];
+        out[3 * i + 1] = s[i];
+        out[3 * i + 2] = b[i];
     }
     #pragma unroll
     for (int k = 0; k < 3; ++k) out[9 + k] = dg[k] - ag[k];
