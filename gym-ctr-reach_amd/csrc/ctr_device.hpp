@@ -269,6 +269,22 @@ __device__ __forceinline__ Trig trig_of(const double al[3])
     return t;
 }
 
+// One sincos from the workgroup's LDS table (<= 2 ulp like sincos_cw), the exact path beyond the
+// table's |x| < 2^20 range.
+__device__ __forceinline__ void sincos_lds(double x, double &s, double &c)
+{
+#ifndef CTR_TRIG_POLY
+    ctr_math::sincos_tab(x, s_trig_tab, s, c);
+#else
+    ctr_math::sincos_fast(x, s, c);
+#endif
+    if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(x)) != 0, 0) && ctr_math::sincos_needs_slow(x)) {
+        const ctr_math::SinCos r = ctr_math::sincos_slow(x);
+        s = r.s;
+        c = r.c;
+    }
+}
+
 // Wave-uniform: does some lane start the FK with an angle of magnitude >= 2^18 (or non-finite)?
 // Otherwise every angle difference met during the FK stays below 2^20: the twist integrated over
 // a backbone (<= ~0.5 m) moves an angle by orders of magnitude less than 2^18 rad.
@@ -916,7 +932,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
     double yR[9];
     {
         double s0, c0;
-        ctr_math::sincos_cw(ya[0], &s0, &c0);
+        sincos_lds(ya[0], s0, c0);
         yR[0] = c0; yR[1] = -s0; yR[2] = 0.0;
         yR[3] = s0; yR[4] = c0;  yR[5] = 0.0;
         yR[6] = 0.0; yR[7] = 0.0; yR[8] = 1.0;
@@ -1095,7 +1111,7 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     join(std::integral_constant<int, 4>{});
     // Y = [Rz(alpha_0) | 0] times the product: r = Rz(alpha_0) m  (model.py:57-60)
     double s0, c0;
-    ctr_math::sincos_cw(ya[0], &s0, &c0);
+    sincos_lds(ya[0], s0, c0);
     tip[0] = fma(-s0, am[1], c0 * am[0]);
     tip[1] = fma(c0, am[1], s0 * am[0]);
     tip[2] = am[2];
