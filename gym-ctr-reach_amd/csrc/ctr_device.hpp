@@ -1051,13 +1051,100 @@ __device__ __forceinline__ double dpp_down(double x)
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// seg_build for an 8-lane group that shares one env (Segment.py:6-61): the group ranks its 10
+// points between its lanes (lane j ranks points j and j + 8) and passes the sorted values and the
+// argsort positions through LDS, instead of every lane running the 45-comparator network.  The
+// rank of point i by (value, index) is its place in the network's stable order, so the sorted
+// values, positions and gap lengths are the network's bit for bit.  A NaN point (no total order)
+// takes the network.  Every lane of the wave must call it.
+__shared__ double s_gsort[CTR_BLOCK / SEG_GROUP][10];
+__shared__ uint8_t s_gpos[CTR_BLOCK / SEG_GROUP][16];
+
+__device__ __forceinline__ Seg seg_build_group(const ctr_system_t &sy, const double beta[3], double *end_lds, int j)
+{
+#pragma clang fp contract(off)
+    double v[10];
+    v[0] = 0.0;
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double dtip = sy.L[i] + beta[i];    // Segment.py:11-12
+        v[1 + i] = beta[i];
+        v[4 + i] = dtip - sy.Lc[i];
+        v[7 + i] = dtip;
+    }
+    bool nan = false;
+    #pragma unroll
+    for (int i = 1; i < 10; ++i) nan |= v[i] != v[i];
+    if (__ballot(nan) != 0) return seg_build(sy, beta, end_lds);
+    const int g = threadIdx.x / SEG_GROUP;
+    // point j (0..7) and point 8 + j (lanes 0 and 1)
+    double va = v[0];
+    #pragma unroll
+    for (int m = 1; m < SEG_GROUP; ++m) va = (j == m) ? v[m] : va;
+    const double vb = (j == 0) ? v[8] : v[9];
+    int ra = 0, rb = 0;
+    #pragma unroll
+    for (int m = 0; m < 10; ++m) {
+        ra += (v[m] < va || (v[m] == va && m < j)) ? 1 : 0;
+        rb += (v[m] < vb || (v[m] == vb && m < 8 + j)) ? 1 : 0;
+    }
+    s_gsort[g][ra] = va;
+    s_gpos[g][j] = (uint8_t)ra;
+    if (j < 2) {
+        s_gsort[g][rb] = vb;
+        s_gpos[g][8 + j] = (uint8_t)rb;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    #pragma unroll
+    for (int k = 0; k < 10; ++k) v[k] = s_gsort[g][k];
+    double len[9];
+    uint32_t zero = 0;                    // bit k: gap k floored to zero length
+    #pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        len[k] = 1e-5 * floor(1e5 * (v[k + 1] - v[k]));   // Segment.py:16
+        zero |= (len[k] == 0.0) ? (1u << k) : 0u;
+    }
+    auto zero_at = [&](int x) { return ((zero >> x) & 1u) != 0u; };
+    uint64_t pc = 0;
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {         // as seg_build (Segment.py:29-36)
+        int a = s_gpos[g][i + 1], b = s_gpos[g][i + 4], c = s_gpos[g][i + 7];
+        if (zero_at(a)) a += 1;
+        if (zero_at(b)) b += 1;
+        if (zero_at(a)) a += 1;
+        if (c <= 8 && zero_at(c)) c += 1;
+        const uint32_t upto_c = (1u << c) - 1u;
+        const uint32_t pres = upto_c & ~((1u << a) - 1u) & 0x1FFu;
+        const uint32_t curv = upto_c & ~((1u << b) - 1u) & 0x1FFu;
+        pc |= ((uint64_t)pres << (9 * i)) | ((uint64_t)curv << (27 + 9 * i));
+    }
+    const double bmin = fmin(fmin(beta[0], beta[1]), beta[2]);
+    Seg sg;
+    sg.kept = 0;
+    sg.pc = pc;
+    double cum = 0.0;
+    #pragma unroll
+    for (int k = 0; k < 9; ++k) {         // Segment.py:46-55
+        cum += len[k];
+        end_lds[k * CTR_BLOCK] = cum + bmin;
+        sg.kept |= ((len[k] != 0.0) && (cum + bmin > 0.0)) ? (1u << k) : 0u;
+    }
+    return sg;
+}
+
 template <bool HAS_UY, bool CAREFUL>
 __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double tip[3], FkStats &st,
                                 double steps_per_m)
 {
     const double beta[3] = {q[0], q[1], q[2]};
     double *end_lds = &s_seg_end[0][threadIdx.x];
+#ifdef CTR_GROUP_SORT_NETWORK
     const Seg sg = seg_build(sy, beta, end_lds);
+#else
+    const Seg sg = seg_build_group(sy, beta, end_lds, j);
+#endif
     const double ya[3] = {q[3], q[4], q[5]};
     const double yu[3] = {0.0, 0.0, 0.0};
     const Trig tconst = trig_of<CAREFUL>(ya);

@@ -76,6 +76,47 @@ def test_step_modes_vs_oracle(cuda, oracle_mod, integrator, spm, model):
             break
 
 
+def test_rigid_group_step_edge_joints(cuda, oracle_mod, golden_dir):
+    """configs[1]'s step runs one env on 8 lanes, which rank the 10 segment points between them
+    (seg_build_group) instead of sorting them each.  Edge joints (fk_edge.npz: ties, limits,
+    reversed sub-um spans) under zero, +max, -max and mixed-sign max actions, which drive joints
+    onto the action-box limits (ties with 0 and between tubes): joints, reward and done
+    bit-exact, tips within 1e-11 m of the oracle, equal RHS counts."""
+    import os
+    import torch
+    from ctr_reach_amd import CtrReachVecEnv
+    d = np.load(os.path.join(golden_dir, "fk_edge.npz"))
+    q0, s0 = d["joints"], d["system"].astype(np.int32)
+    m = len(q0)
+    env0 = CtrReachVecEnv(1, device=cuda)
+    hi = env0.action_space.high
+    signs = np.array([[0, 0, 0, 0, 0, 0], [1, 1, 1, 1, 1, 1], [-1, -1, -1, -1, -1, -1],
+                      [1, -1, 1, -1, 1, -1], [-1, 1, -1, 1, -1, 1]], np.float32)
+    q = np.tile(q0, (len(signs), 1))
+    sysid = np.tile(s0, len(signs))
+    a = (np.repeat(signs, m, axis=0) * hi).astype(np.float32)
+    n = len(q)
+    env = CtrReachVecEnv(n, device=cuda, seed=9, select_systems=[0, 1, 2, 3], autoreset=False,
+                         integrator="rk4", rk4_steps_per_m=100, model="rigid")
+    env.enable_nfev()
+    env.reset()
+    env.joints.copy_(torch.tensor(q, device=cuda))
+    env.system.copy_(torch.tensor(sysid, device=cuda))
+    for _ in range(3):
+        qi = env.joints.cpu().numpy()
+        dg = env.desired_goal.cpu().numpy()
+        t = env.t.cpu().numpy()
+        obs, rew, done, info = env.step(torch.tensor(a, device=cuda))
+        torch.cuda.synchronize()
+        ref = oracle_mod.step(qi, a, dg, t, env.goal_tolerance.get_tol(), system=sysid, multi=True,
+                              integrator="rk4", steps_per_m=100, model="rigid")
+        np.testing.assert_array_equal(env.joints.cpu().numpy(), ref["joints"])
+        assert np.abs(env.achieved_goal.cpu().numpy() - ref["achieved_goal"]).max() < 1e-11
+        np.testing.assert_array_equal(rew.cpu().numpy(), ref["reward"].astype(np.float32))
+        np.testing.assert_array_equal(done.cpu().numpy(), ref["done"])
+        np.testing.assert_array_equal(env.nfev.cpu().numpy(), ref["nfev"])
+
+
 def test_reset_goals_follow_mode(cuda, oracle_mod):
     """Reset goals are the FK of the drawn joints under the env's own solver mode."""
     import torch
