@@ -1224,8 +1224,10 @@ __device__ __forceinline__ void set_action_lane(const ctr_system_t &sy, bool con
         else if (constrain_alpha) { lo = -3.14159274101257324f; hi = 3.14159274101257324f; }
         else { lo = -INFINITY; hi = INFINITY; }
         float v = q[i] + a[i];
-        v = v < lo ? lo : v;
-        v = v > hi ? hi : v;
+        if (i < 3 || constrain_alpha) {   // the +-inf bounds clamp nothing (NaN included)
+            v = v < lo ? lo : v;
+            v = v > hi ? hi : v;
+        }
         q[i] = v;
     }
     #pragma unroll
@@ -1236,6 +1238,17 @@ __device__ __forceinline__ void set_action_lane(const ctr_system_t &sy, bool con
         const float z = d + yv;
         q[i - 1] = (z > m) ? z : m;                              // max(., L_i - L_{i-1} + b[i])
     }
+}
+
+// The step's n_substeps set_action passes (ctr_reach_env.py:133-135).  The constrain_alpha test is
+// taken once, outside the loop, so the unconstrained case runs without the angle clamps.
+__device__ __forceinline__ void set_action_substeps(const ctr_system_t &sy, bool constrain_alpha, int n, float q[6],
+                                                    const float a[6])
+{
+    if (constrain_alpha)
+        for (int k = 0; k < n; ++k) set_action_lane(sy, true, q, a);
+    else
+        for (int k = 0; k < n; ++k) set_action_lane(sy, false, q, a);
 }
 
 // obs.py:136-164.  Writes obs_dim (13 or 14) values in float64, the reference's dtype; the env

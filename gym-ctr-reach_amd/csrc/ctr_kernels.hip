@@ -396,7 +396,7 @@ __global__ __launch_bounds__(BLOCK) void k_set_action(KCfg kc, float *__restrict
     #pragma unroll
     for (int i = 0; i < 6; ++i) { q[i] = joints[6 * e + i]; a[i] = actions[6 * e + i]; }
     const int s = sys_idx ? clamp_sys(sys_idx[e], kc.c.n_systems) : 0;
-    for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(s_sys[s], kc.c.constrain_alpha != 0, q, a);
+    set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
     #pragma unroll
     for (int i = 0; i < 6; ++i) joints[6 * e + i] = q[i];
 }
@@ -571,7 +571,7 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             float a[6];
             #pragma unroll
             for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
-            for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(s_sys[s], kc.c.constrain_alpha != 0, q, a);
+            set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
         }
         PoolPre pp;
         if (live) pool_prefetch(kc, b, e, autoreset, pp);
@@ -592,7 +592,7 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
         PoolPre pp;
         pool_prefetch(kc, b, e, autoreset, pp);
-        for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(sy, kc.c.constrain_alpha != 0, q, a);
+        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
         FkStats st = {0, 0, 0, 0, 0};
         double ag[3];
 #ifdef CTR_EXP_NOFK
@@ -659,7 +659,7 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
             float a[6];
             #pragma unroll
             for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
-            for (int k = 0; k < kc.c.n_substeps; ++k) set_action_lane(s_sys[s], kc.c.constrain_alpha != 0, q, a);
+            set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
         }
         const SysK &sy = live ? episode_sys_at(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e), lane)
                               : s_sys[0];
