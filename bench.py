@@ -299,6 +299,15 @@ def main():
         g.manual_seed(args.seed + 17 + rank)
         env.t.copy_(torch.randint(0, max_steps, (n,), generator=g, dtype=torch.int32))
     acts = make_actions(env, 8, args.seed + rank)
+    if gather:
+        # the env steps on a high-priority stream, RCCL's gather on its normal-priority one.  The
+        # gather kernel (248-256 VGPRs, 37 KB LDS per workgroup) cannot share a SIMD with a k_step
+        # wave (384 of the 512 registers), so whichever is dispatched first holds the CU: with the
+        # step first, the gather of step t fills the CUs the slowest waves of step t+1 leave idle
+        # instead of keeping step t+1's workgroups off the CUs it took
+        hp = torch.cuda.Stream(device=dev, priority=-1)
+        hp.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(hp)
     stream = torch.cuda.current_stream()
     works = [None, None]
 
