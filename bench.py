@@ -17,8 +17,8 @@ consumed.  resets_in_window and refills_in_window are reported.
 Multi-GPU: ``python bench.py --gpus N`` launches N ranks itself (one process per GPU, before
 anything touches a GPU); under ``torch.distributed.run`` the ranks come from the environment.
 Rank r owns the contiguous global env ids [r n, (r + 1) n) (weak scaling, no collective on the
-step itself).  With N > 1 every timed step also all-gathers the packed step outputs (20 B/env:
-tip, reward, done | success) over RCCL -- BASELINE configs[3] -- asynchronously on RCCL's
+step itself).  With N > 1 every timed step also all-gathers the packed step outputs (16 B/env:
+tip, done | success | reward) over RCCL -- BASELINE configs[3] -- asynchronously on RCCL's
 stream while the next step runs; k_step writes the packed rows itself (pack_outputs).  A
 barrier + device sync bracket the timed region and the time is the MAX over ranks.
 
@@ -413,7 +413,7 @@ def main():
                    "rk4_steps_per_m": cfgd["rk4_steps_per_m"] if cfgd["integrator"] == "rk4" else None,
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
                    "process_group": {"backend": backend, "world_size": ws} if dist else None,
-                   "all_gather": {"bytes_per_env": 20, "async": True} if gather else None,
+                   "all_gather": {"bytes_per_env": 4 * D.PACK_WIDTH, "async": True} if gather else None,
                    "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,
                                   "autoreset": "pooled (no miss sweep)" if env.pool_depth >= env.refill_interval
                                   else "pooled + miss sweep"},

@@ -470,12 +470,11 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
     uint32_t stat = st.status;
     if (o.nfev) o.nfev[e] = st.nfev;
     if (o.packed) {
-        // the gather row of this step (distributed.PACK_WIDTH): the pre-reset tip, so a done env
-        // reports where its episode ended
-        float *pk = o.packed + 5 * e;
-        pk[0] = (float)ag[0]; pk[1] = (float)ag[1]; pk[2] = (float)ag[2];
-        pk[3] = reward;
-        pk[4] = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0));
+        // the gather row of this step (distributed.PACK_WIDTH, one 16-B store): the pre-reset tip,
+        // so a done env reports where its episode ended, and done | success << 1 | (reward = -1)
+        // << 2 (the sparse reward is -1 or 0, ctr_reach_env.py:169)
+        const float fl = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0) | ((reward < 0.0f) ? 4 : 0));
+        *reinterpret_cast<float4 *>(o.packed + 4 * e) = make_float4((float)ag[0], (float)ag[1], (float)ag[2], fl);
     }
     // ctr_step_her: the transition goes into the env's HER episode before any auto-reset
     if (her) {

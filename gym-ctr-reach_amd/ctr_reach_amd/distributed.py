@@ -3,13 +3,13 @@
 Environments are independent, so the step itself has no exchange: rank r owns the contiguous
 global ids [r * n, (r + 1) * n) (``env_base``) and every random draw is keyed by the global id,
 which makes results independent of the number of GPUs.  The only collective is OPTIONAL and off
-the data path: ``all_gather_outputs`` packs (tip x/y/z, reward, done | success << 1) into 20 B per
-env and all-gathers it over RCCL (backend "nccl" on ROCm, xGMI between the GPUs of a node) for a
+the data path: ``all_gather_outputs`` packs (tip x/y/z, done | success << 1 | (reward = -1) << 2)
+into 16 B per env and all-gathers it over RCCL (backend "nccl" on ROCm, xGMI between the GPUs of a node) for a
 single-process trainer that wants every shard's outputs.
 """
 import os
 
-PACK_WIDTH = 5   # float32 words per env: tip x, y, z, reward, flags (done | success << 1)
+PACK_WIDTH = 4   # float32 words per env: tip x, y, z, flags (done | success << 1 | (reward = -1) << 2)
 
 
 def world():
@@ -24,25 +24,27 @@ def shard(num_envs_per_rank, rank):
 
 
 def pack_step_outputs(achieved_goal, reward, done, success, out=None):
-    """[n, 5] float32 tensor: tip (3, f64 -> f32), reward, done | success << 1."""
+    """[n, 4] float32 tensor: tip (3, f64 -> f32), done | success << 1 | (reward = -1) << 2.
+    The env's reward is sparse, -1 or 0 (ctr_reach_env.py:160-170), so one bit carries it."""
     import torch
     n = achieved_goal.shape[0]
     if out is None:
         out = torch.empty((n, PACK_WIDTH), dtype=torch.float32, device=achieved_goal.device)
     out[:, 0:3] = achieved_goal
-    out[:, 3] = reward
-    out[:, 4] = done.to(torch.float32) + 2.0 * success.to(torch.float32)
+    out[:, 3] = done.to(torch.float32) + 2.0 * success.to(torch.float32) + 4.0 * (reward < 0).to(torch.float32)
     return out
 
 
 def unpack_step_outputs(packed):
+    """(tip [n, 3] f32, reward [n] f32, done [n] bool, success [n] bool) of packed rows."""
     import torch
-    flags = packed[:, 4].round().to(torch.int32)
-    return packed[:, 0:3], packed[:, 3], (flags & 1).bool(), (flags & 2).bool()
+    flags = packed[:, 3].round().to(torch.int32)
+    reward = ((flags >> 2) & 1).to(torch.float32).neg_().add_(0.0)     # -1 or +0 (not -0)
+    return packed[:, 0:3], reward, (flags & 1).bool(), (flags & 2).bool()
 
 
 def all_gather_outputs(packed, group=None, async_op=False):
-    """All-gather every rank's packed [n, 5] block into [world * n, 5] (rank-major = global id
+    """All-gather every rank's packed [n, 4] block into [world * n, 4] (rank-major = global id
     order).  Uses all_gather_into_tensor: one RCCL ring/tree call for the whole step.
 
     async_op=True returns (out, work): the collective runs on RCCL's own stream, ordered after

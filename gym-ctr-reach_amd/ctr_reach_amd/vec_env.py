@@ -19,6 +19,7 @@ so results do not depend on how environments are sharded over GPUs.
 import numpy as np
 
 from . import _abi
+from . import distributed as D
 from .goal_tolerance import GoalTolerance
 from .spaces import Box, Dict
 from .systems import default_kwargs, make_config, solver_codes, tubes_from_params
@@ -155,10 +156,10 @@ class CtrReachVecEnv(object):
         self.terminal_achieved = torch.zeros((n, 3), dtype=f64, device=dev)
         self.status = torch.zeros(n, dtype=i32, device=dev)
         self.nfev = None
-        # pack_outputs: k_step also writes each step's gather row ([n, 5] f32, distributed.PACK_WIDTH)
+        # pack_outputs: k_step also writes each step's gather row ([n, 4] f32, distributed.PACK_WIDTH)
         # into one of two alternating buffers, so gather_outputs() needs no packing launch and one
         # gather may stay in flight while the next step writes the other buffer
-        self.packed_bufs = [torch.zeros((n, 5), dtype=f32, device=dev) for _ in range(2)] if pack_outputs else None
+        self.packed_bufs = [torch.zeros((n, D.PACK_WIDTH), dtype=f32, device=dev) for _ in range(2)] if pack_outputs else None
         self._packed_k = 0
         self.refills = 0          # ctr_pool_refill launches so far (bench accounting)
         self.sweeps = 0           # steps that launched the auto-reset miss sweep (CTR_AUTORESET_SWEEP)
@@ -450,7 +451,7 @@ class CtrReachVecEnv(object):
 
     def gather_outputs(self, group=None, async_op=False):
         """Optional collective for a single-process trainer: every rank's last-step (tip, reward,
-        done, success) packed to 20 B/env and all-gathered over RCCL -> [world * n, 5] float32
+        done, success) packed to 16 B/env and all-gathered over RCCL -> [world * n, 4] float32
         in global-id order.  Not used on the stepping path.  async_op=True returns (out, work)
         and lets the next step() run while the gather is in flight (RCCL's stream); the pack
         buffers alternate, so one gather may be outstanding per env.
@@ -458,7 +459,6 @@ class CtrReachVecEnv(object):
         With ``pack_outputs=True`` the step kernel itself wrote the packed rows (no packing
         launch); otherwise they are packed here from the step's outputs."""
         import torch
-        from . import distributed as D
         if self.packed_bufs is not None:
             return D.all_gather_outputs(self.packed_bufs[self._packed_k], group=group, async_op=async_op)
         d = self.done.bool()
@@ -470,7 +470,7 @@ class CtrReachVecEnv(object):
         return D.all_gather_outputs(bufs[k], group=group, async_op=async_op)
 
     def packed_outputs(self):
-        """The last step's packed rows ([n, 5] float32, see gather_outputs); needs pack_outputs=True."""
+        """The last step's packed rows ([n, 4] float32, see gather_outputs); needs pack_outputs=True."""
         if self.packed_bufs is None:
             raise RuntimeError("packed_outputs() needs CtrReachVecEnv(..., pack_outputs=True)")
         return self.packed_bufs[self._packed_k]

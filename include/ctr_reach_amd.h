@@ -177,11 +177,12 @@ typedef struct ctr_step_out_t {
     double   *terminal_achieved; /* [n][3] or NULL: achieved goal of the terminal step           */
     uint32_t *status;            /* [n] or NULL: CTR_STATUS_* bits                               */
     uint32_t *nfev;              /* [n] or NULL: RHS evaluations spent in the step's FK          */
-    float    *packed;            /* [n][5] or NULL: the step's outputs packed for the optional
-                                    all-gather of a single-process trainer: tip x, y, z (float32;
-                                    the terminal achieved goal of a done env), reward,
-                                    done | success << 1 (as a float).  Written by k_step itself,
-                                    so gathering costs no packing launch.                         */
+    float    *packed;            /* [n][4] (16-B aligned) or NULL: the step's outputs packed for
+                                    the optional all-gather of a single-process trainer: tip x, y,
+                                    z (float32; the terminal achieved goal of a done env) and
+                                    done | success << 1 | (reward == -1) << 2 as a float (the
+                                    reward is -1 or 0).  Written by k_step itself, so gathering
+                                    costs no packing launch.                                      */
 } ctr_step_out_t;
 
 /* ---------------------------------------------------------------------------------------

@@ -65,7 +65,8 @@ def test_two_rank_shards_match_single_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert t == 1.5                         # max over ranks
-    assert full.shape == (world * n, 5)
+    from ctr_reach_amd import distributed as D
+    assert full.shape == (world * n, D.PACK_WIDTH)
     # the same global envs stepped in ONE process
     N = world * n
     qd, _ = oracle.sample_joints(N, seed=99, stream=0, epoch=1, env_base=0)
@@ -77,8 +78,9 @@ def test_two_rank_shards_match_single_process():
         acts.append((rng.uniform(-1, 1, (n, 6)) * np.array([1e-3] * 3 + [0.087] * 3)).astype(np.float32))
     ref = oracle.step(q0, np.concatenate(acts), dg, 0, 0.05)
     np.testing.assert_allclose(full[:, :3], ref["achieved_goal"].astype(np.float32))
-    np.testing.assert_array_equal(full[:, 3], ref["reward"].astype(np.float32))
-    flags = full[:, 4].astype(int)
+    _, rew, _, _ = D.unpack_step_outputs(torch.tensor(full))
+    np.testing.assert_array_equal(rew.numpy(), ref["reward"].astype(np.float32))
+    flags = full[:, 3].astype(int)
     np.testing.assert_array_equal(flags & 1, ref["done"].astype(int))
     np.testing.assert_array_equal((flags >> 1) & 1, ref["is_success"].astype(int))
 

@@ -31,7 +31,8 @@ def _packed_want(env):
     import torch
     d = env.done.bool()
     tip = torch.where(d[:, None], env.terminal_achieved, env.achieved_goal).float()
-    return torch.cat([tip, env.reward[:, None], (env.done.float() + 2 * env.success.float())[:, None]], 1)
+    flags = env.done.float() + 2 * env.success.float() + 4 * (env.reward < 0).float()
+    return torch.cat([tip, flags[:, None]], 1)
 
 
 def test_configs3_eight_shards_match_one_batch(cuda):
@@ -129,5 +130,5 @@ def test_bench_two_ranks_gloo_rehearsal(cuda):
                  env={"CTR_BENCH_BACKEND": "gloo", "CTR_BENCH_SAME_DEVICE": "1"})
     assert out["n_gpus"] == 2 and out["config"]["global_envs"] == 4096
     assert out["config"]["process_group"] == {"backend": "gloo", "world_size": 2}
-    assert out["config"]["all_gather"]["bytes_per_env"] == 20
+    assert out["config"]["all_gather"]["bytes_per_env"] == 16
     assert out["config"]["steady_state"]["refills_in_window"] == 2

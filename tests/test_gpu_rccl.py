@@ -2,8 +2,8 @@
 in a one-rank process group (the multi-rank logic is covered with gloo in test_distributed.py):
 synchronous and overlapped (async_op) forms, and a step launched while the gather is in flight.
 
-Bars: the gathered block equals the env's own (tip as float32, reward, done | success << 1)
-bit for bit."""
+Bars: the gathered block equals the env's own (tip as float32, done | success << 1 |
+(reward = -1) << 2) bit for bit, and unpacks to the env's reward / done / success."""
 import os
 import socket
 
@@ -19,6 +19,17 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _want(env, tip):
+    """The packed rows of the env's last step (distributed.PACK_WIDTH), checked against unpack."""
+    import torch
+    from ctr_reach_amd import distributed as D
+    flags = env.done.float() + 2 * env.success.float() + 4 * (env.reward < 0).float()
+    want = torch.cat([tip, flags[:, None]], 1)
+    t, r, d, sc = D.unpack_step_outputs(want)
+    assert torch.equal(r, env.reward) and torch.equal(d, env.done.bool()) and torch.equal(sc, env.success.bool())
+    return want
 
 
 def test_gather_outputs_over_rccl(cuda):
@@ -39,7 +50,7 @@ def test_gather_outputs_over_rccl(cuda):
         full = env.gather_outputs()
         d = env.done.bool()
         tip = torch.where(d[:, None], env.terminal_achieved, env.achieved_goal).float()
-        want = torch.cat([tip, env.reward[:, None], (env.done.float() + 2 * env.success.float())[:, None]], 1)
+        want = _want(env, tip)
         assert torch.equal(full, want)
         # overlapped: the gather of step k runs while step k + 1 is launched
         out, work = env.gather_outputs(async_op=True)
@@ -70,7 +81,7 @@ def test_gather_of_kernel_packed_rows_over_rccl(cuda):
             env.step(act)
             d = env.done.bool()
             tip = torch.where(d[:, None], env.terminal_achieved, env.achieved_goal).float()
-            want = torch.cat([tip, env.reward[:, None], (env.done.float() + 2 * env.success.float())[:, None]], 1)
+            want = _want(env, tip)
             out, work = env.gather_outputs(async_op=True)
             env.step(act)                      # writes the other pack buffer while the gather runs
             work.wait()
