@@ -89,6 +89,16 @@ if step:
                   "counts in k_step's own row-load / row-store shapes (%s_traffic_calibration.json)" % tag)
          if cal else "FETCH_SIZE doubled per the gfx950 calibration for wide reads (uncalibrated here)",
          "avg_ns_rocprof": avg_ns.get(step[0])}
+    # the bench's own k_step timing set: its last 32 launches (auto-reset off, after 256 untimed
+    # ones), which bench.py brackets with one HIP event pair -- the same launches, rocprof's clock
+    trace = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        ks = sorted((r for r in csv.DictReader(open(trace)) if step[0] in r["Kernel_Name"]),
+                    key=lambda r: int(r["Start_Timestamp"]))
+        dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ks]
+        if len(dur) >= 32:
+            t["avg_ns_rocprof_bench_timed_32"] = sum(dur[-32:]) / 32.0
+            t["launches_in_trace"] = len(dur)
     with open(os.path.join(dst, "traffic.json"), "w") as fh:
         json.dump(t, fh, indent=1)
     print(json.dumps(t, indent=1))
