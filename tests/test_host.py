@@ -214,3 +214,23 @@ def test_her_abi_rejects_bad_arguments_without_gpu():
     h.strategy, h.n = 0, 8
     assert lib.ctr_her_sample(h, 4, 0, 0, _abi.CtrHerBatch(), None) == -1 and b"buffer" in lib.ctr_last_error()
     assert lib.ctr_her_sample(None, 4, 0, 0, _abi.CtrHerBatch(), None) == -1
+
+
+def test_gather_row_pack_roundtrip():
+    """The 16-B gather row (distributed.PACK_WIDTH = 4 float32 words): tip rounded to float32,
+    and done / success / (reward = -1) as flag bits; the env's sparse reward (-1 or 0,
+    ctr_reach_env.py:160-170) comes back exactly, with +0 rather than -0."""
+    import torch
+    from ctr_reach_amd import distributed as D
+    rng = np.random.default_rng(0)
+    n = 1000
+    tip = torch.tensor(rng.normal(0, 0.1, (n, 3)))
+    reward = torch.tensor(-(rng.random(n) < 0.7).astype(np.float32))
+    done = torch.tensor(rng.random(n) < 0.3).to(torch.uint8)
+    success = (reward == 0).to(torch.uint8)
+    p = D.pack_step_outputs(tip, reward, done, success)
+    assert p.shape == (n, D.PACK_WIDTH) and p.dtype == torch.float32 and p.element_size() * D.PACK_WIDTH == 16
+    t2, r2, d2, s2 = D.unpack_step_outputs(p)
+    assert torch.equal(t2, tip.float())
+    assert torch.equal(r2, reward) and not torch.signbit(r2[r2 == 0]).any()
+    assert torch.equal(d2, done.bool()) and torch.equal(s2, success.bool())
