@@ -418,17 +418,7 @@ struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
 
-#ifdef CTR_DIAG_TIME
-__device__ __forceinline__ uint64_t stamp()
-{
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define CTR_STAMP(var) const uint64_t var = stamp()
-#elif defined(CTR_ASM_MARKERS)
+#if defined(CTR_ASM_MARKERS)
 // asm-listing build: a comment + scheduling barrier at each block boundary (instruction counts)
 #define CTR_STAMP(var)                                   \
     do {                                                 \
@@ -502,18 +492,8 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
     bool sh_rev = false;
     int sh_j = 0;                                   // SHAPE: next t_eval point of the segment
 
-#ifdef CTR_DIAG_TIME
-    uint64_t c_init = 0, c_stage = 0, c_tail = 0;
-    CTR_STAMP(t_begin);
-#endif
     for (;;) {
         CTR_STAMP(ts0);
-#ifdef CTR_DIAG_WAVE
-        // diagnostic build: wave-uniform counts of loop iterations / iterations running the
-        // segment-start block (reported in place of nrej / nseg)
-        st.nrej++;
-        if (__ballot(need_init && remaining != 0)) st.nseg++;
-#endif
         if (need_init) {
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
@@ -543,9 +523,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             double fr[3];
             stage_at<false>(p, ty, yu, yR, f, fr);
             st.nfev++;
-#ifndef CTR_DIAG_WAVE
             st.nseg++;
-#endif
             const double interval = tb - t0;
             if (interval == 0.0) {                                // OdeSolver.step: t == t_bound
                 if (SHAPE)                                        // ConstantDenseOutput(y)
@@ -762,11 +740,6 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         // error_norm ** -0.2 = (error_norm^2) ** -0.1
         const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
         CTR_STAMP(ts3);
-#ifdef CTR_DIAG_TIME
-        c_init += ts1 - ts0;
-        c_stage += ts2 - ts1;
-        c_tail += ts3 - ts2;
-#endif
         if (en2n < 1.0) {
             double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
@@ -804,18 +777,9 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         } else {
             ha *= fmax(0.2, fpow);
             rejected = true;
-#ifndef CTR_DIAG_WAVE
             st.nrej++;
-#endif
         }
     }
-#ifdef CTR_DIAG_TIME
-    CTR_STAMP(t_end);
-    st.nfev = (uint32_t)c_init;
-    st.nstep = (uint32_t)c_stage;
-    st.nrej = (uint32_t)c_tail;
-    st.nseg = (uint32_t)(t_end - t_begin);
-#endif
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 #undef CTR_FAL

@@ -29,9 +29,6 @@
 
 #include "ctr_device.hpp"
 #include "ctr_reach_amd.h"
-#ifdef CTR_PAIR
-#include "ctr_pair.hpp"
-#endif
 
 using namespace ctr;
 
@@ -119,20 +116,6 @@ __device__ __forceinline__ const SysK &episode_sys(const KCfg &kc, const SysK *s
     me.lut = nullptr;
     return me;
 }
-
-#ifdef CTR_PAIR
-// As episode_sys, with the lane's dynamic-LDS slot given (the pair kernels: 64 slots, wave A).
-__device__ __forceinline__ const SysK &episode_sys_at(const KCfg &kc, const SysK *s_sys, const ctr_tube_raw_t *s_raw,
-                                                      int s, uint32_t epoch, uint64_t genv, int slot)
-{
-    if (kc.c.domain_rand == 0.0 || epoch == 0) return s_sys[s];
-    SysK &me = s_lane_dyn[slot];
-    domain_system(s_sys[s], s_raw[s], kc.c.domain_rand, kc.c.seed, epoch, genv, me, nullptr);
-    #pragma unroll
-    for (int j = 0; j < 11; ++j) sysk_derive(me, j);
-    return me;
-}
-#endif  // CTR_PAIR
 
 // MODE bits: 1 = some tube has y pre-curvature, 2 = fixed-step RK4 (else scipy RK45),
 // 4 = torsionally rigid model.
@@ -245,60 +228,6 @@ __global__ __launch_bounds__(BLOCK) void k_fk(KCfg kc, const float *__restrict__
     if (status) status[e] = st.status;
 }
 
-
-#ifdef CTR_PAIR
-// The reference's configuration (scipy RK45, torsionally compliant: MODE 0 / 1) on wave pairs
-// (ctr_pair.hpp): 64 envs per 128-thread workgroup, wave A (u_z, alpha, trig, control) and
-// wave B (R, r), two waves per SIMD.  tables != NULL: per-row tube tables as in k_fk.
-template <int MODE>
-__global__ __launch_bounds__(PAIR_BLOCK, 2) void k_fk_pair(KCfg kc, const float *__restrict__ joints,
-                                                           const int32_t *__restrict__ sys_idx,
-                                                           const ctr_system_t *__restrict__ tables, int64_t n,
-                                                           double *__restrict__ tip, uint32_t *__restrict__ stats,
-                                                           uint32_t *__restrict__ status)
-{
-    static_assert((MODE & 6) == 0, "pair FK: scipy RK45, compliant model");
-    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
-    __shared__ PairLds X;
-    stage_systems(kc, s_sys);
-    const int lane = threadIdx.x & (PAIR_LANES - 1);
-    const int64_t e = (int64_t)blockIdx.x * PAIR_LANES + lane;
-    const bool live = e < n;
-    if (threadIdx.x >= PAIR_LANES) {
-        fk_pair_B(X);
-        return;
-    }
-    double q[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    const SysK *sy = &s_sys[0];
-    if (live) {
-        #pragma unroll
-        for (int i = 0; i < 6; ++i) q[i] = (double)joints[6 * e + i];    // model.py:48-62
-        sy = &s_sys[sys_idx ? clamp_sys(sys_idx[e], kc.c.n_systems) : 0];
-        if (tables) {
-            SysK &me = s_lane_dyn[lane];
-            static_cast<ctr_system_t &>(me) = tables[e];
-            #pragma unroll
-            for (int j = 0; j < 11; ++j) sysk_derive(me, j);
-            sy = &me;
-        }
-    }
-    FkStats st = {0, 0, 0, 0, 0};
-    double out[3];
-    if (fk_needs_careful_trig(q)) fk_pair_A<(MODE & 1) != 0, true>(*sy, q, live, out, st, X);
-    else fk_pair_A<(MODE & 1) != 0, false>(*sy, q, live, out, st, X);
-    if (!live) return;
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) tip[3 * e + i] = out[i];
-    if (stats) {
-        stats[4 * e + 0] = st.nfev;
-        stats[4 * e + 1] = st.nstep;
-        stats[4 * e + 2] = st.nrej;
-        stats[4 * e + 3] = st.nseg;
-    }
-    if (status) status[e] = st.status;
-}
-
-#endif  // CTR_PAIR
 
 // Backbone shape (model.py:66-68, 119-174): the FK plus r at the 30 t_eval points of every
 // segment from the RK45 dense output.  Row e writes r[e][cap][3], s[e][cap], npts[e].
@@ -594,11 +523,7 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
         FkStats st = {0, 0, 0, 0, 0};
         double ag[3];
-#ifdef CTR_EXP_NOFK
-        ag[0] = q[0]; ag[1] = q[1]; ag[2] = q[2];      // experiment: step overhead without the FK
-#else
         fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);
-#endif
         step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
     }
     if (autoreset) {
@@ -630,77 +555,6 @@ __global__ __launch_bounds__(BLOCK) void k_step_her(KCfg kc, ctr_batch_t b, cons
 {
     step_body<MODE, true>(kc, b, actions, o, autoreset, hk);
 }
-
-#ifdef CTR_PAIR
-// k_step for the reference's configuration (scipy RK45, compliant: MODE 0 / 1) on wave pairs
-// (ctr_pair.hpp): wave A runs the env logic of step_body (set_action, reward, obs, pooled
-// auto-reset, HER recording) and the (u_z, alpha) half of the FK, wave B the (R, r) half.
-template <int MODE, bool HER>
-__device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t &b, const float *__restrict__ actions,
-                                               const ctr_step_out_t &o, int32_t autoreset, const HerK &hk)
-{
-    static_assert((MODE & 6) == 0, "pair step: scipy RK45, compliant model");
-    const ctr_her_t *her = HER ? &hk.h : nullptr;
-    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
-    __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
-    __shared__ PairLds X;
-    stage_systems(kc, s_sys, s_raw);
-    const int lane = threadIdx.x & (PAIR_LANES - 1);
-    const int64_t e = (int64_t)blockIdx.x * PAIR_LANES + lane;
-    const bool isA = threadIdx.x < PAIR_LANES;
-    const bool live = isA && e < b.n;
-    StepFlags fl;
-    if (isA) {
-        int s = 0;
-        float q[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (live) {
-            s = clamp_sys(b.system[e], kc.c.n_systems);
-            float a[6];
-            #pragma unroll
-            for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
-            set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
-        }
-        const SysK &sy = live ? episode_sys_at(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e), lane)
-                              : s_sys[0];
-        const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
-        FkStats st = {0, 0, 0, 0, 0};
-        double ag[3];
-        if (fk_needs_careful_trig(qd)) fk_pair_A<(MODE & 1) != 0, true>(sy, qd, live, ag, st, X);
-        else fk_pair_A<(MODE & 1) != 0, false>(sy, qd, live, ag, st, X);
-        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, PoolPre{});
-    } else {
-        fk_pair_B(X);
-    }
-    if (autoreset) {
-        if (autoreset == CTR_AUTORESET_POOLED) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;
-        } else {
-            const int32_t one[1] = {(int32_t)e};
-            wave_append(miss_counter(b), miss_items(b), b.n, fl.miss, one, 1);
-        }
-        if (b.pool_depth > 0) {
-            const int32_t two[2] = {(int32_t)e, (int32_t)(fl.pooled_r + (uint32_t)b.pool_depth)};
-            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
-        }
-    }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(PAIR_BLOCK, 2) void k_step_pair(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
-                                                             ctr_step_out_t o, int32_t autoreset)
-{
-    step_body_pair<MODE, false>(kc, b, actions, o, autoreset, HerK{});
-}
-
-template <int MODE>
-__global__ __launch_bounds__(PAIR_BLOCK, 2) void k_step_her_pair(KCfg kc, ctr_batch_t b,
-                                                                 const float *__restrict__ actions, ctr_step_out_t o,
-                                                                 int32_t autoreset, HerK hk)
-{
-    step_body_pair<MODE, true>(kc, b, actions, o, autoreset, hk);
-}
-
-#endif  // CTR_PAIR
 
 // ------------------------------------------------------------------------------------------
 // One reset (reset number r of global env genv) computed by a lane PAIR: the even lane draws the
@@ -996,14 +850,6 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
 // Launch kernel template K<MODE> for the runtime mode (8 instantiations).
-#ifdef CTR_AB_MODE0
-// A/B experiment builds: mode 0 only (system-0 headline workload), 8x faster to compile
-#define CTR_LAUNCH(K, MODE, GRID, SHM, STREAM, ...)                                                \
-    do {                                                                                           \
-        if ((MODE) != 0) return fail(CTR_EINVAL, "A/B build: mode 0 only");                      \
-        hipLaunchKernelGGL(K<0>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__);                     \
-    } while (0)
-#else
 #define CTR_LAUNCH(K, MODE, GRID, SHM, STREAM, ...)                                                     \
     do {                                                                                           \
         switch (MODE) {                                                                            \
@@ -1017,30 +863,6 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK)
         default: hipLaunchKernelGGL(K<7>, GRID, dim3(BLOCK), SHM, STREAM, __VA_ARGS__); break;       \
         }                                                                                          \
     } while (0)
-#endif
-
-// The wave-pair kernels (ctr_pair.hpp) are an experiment, built only with -DCTR_PAIR: correct
-// (the GPU suite passes with them), but 118 us against the one-lane k_step's 92 us at 65 536
-// envs (optimisation log).  They cover scipy RK45 + compliant (MODE 0 / 1).
-#ifdef CTR_PAIR
-inline bool use_pair(const KCfg &kc) { return (kc.mode & 6) == 0; }
-
-inline unsigned pair_grid(int64_t n) { return (unsigned)((n + PAIR_LANES - 1) / PAIR_LANES); }
-
-#if defined(CTR_AB_MODE0)
-#define CTR_LAUNCH_PAIR(K, MODE, GRID, SHM, STREAM, ...)                                           \
-    do {                                                                                           \
-        if ((MODE) != 0) return fail(CTR_EINVAL, "A/B build: mode 0 only");                      \
-        hipLaunchKernelGGL(K<0>, GRID, dim3(PAIR_BLOCK), SHM, STREAM, __VA_ARGS__);                \
-    } while (0)
-#else
-#define CTR_LAUNCH_PAIR(K, MODE, GRID, SHM, STREAM, ...)                                           \
-    do {                                                                                           \
-        if ((MODE) == 1) hipLaunchKernelGGL(K<1>, GRID, dim3(PAIR_BLOCK), SHM, STREAM, __VA_ARGS__); \
-        else hipLaunchKernelGGL(K<0>, GRID, dim3(PAIR_BLOCK), SHM, STREAM, __VA_ARGS__);           \
-    } while (0)
-#endif
-#endif  // CTR_PAIR
 
 }  // namespace
 
@@ -1058,13 +880,6 @@ static int fk_impl(const float *joints, const int32_t *sys_idx, const ctr_system
     if (n == 0) return 0;
     KCfg kc = make_kcfg(cfg);
     if (tables) kc.mode |= 1;     // per-row tables may carry y pre-curvature
-#ifdef CTR_PAIR
-    if (use_pair(kc)) {
-        CTR_LAUNCH_PAIR(k_fk_pair, kc.mode, dim3(pair_grid(n)), tables ? (size_t)PAIR_LANES * sizeof(SysK) : 0,
-                        (hipStream_t)stream, kc, joints, sys_idx, tables, n, tip, stats, status);
-        return hip_check("ctr_fk launch");
-    }
-#endif
     CTR_LAUNCH(k_fk, kc.mode, dim3(grid_for(n)), tables ? (size_t)BLOCK * sizeof(SysK) : 0, (hipStream_t)stream, kc,
                joints, sys_idx, tables, n, tip, stats, status);
     return hip_check("ctr_fk launch");
@@ -1152,15 +967,6 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
     HerK hk = {};
     if (her) hk.h = *her;
     const int32_t her_on = her != nullptr;
-#ifdef CTR_PAIR
-    if (use_pair(kc)) {
-        const size_t shm = kc.c.domain_rand != 0.0 ? (size_t)PAIR_LANES * sizeof(SysK) : 0;
-        if (her)
-            CTR_LAUNCH_PAIR(k_step_her_pair, kc.mode, dim3(pair_grid(b.n)), shm, s, kc, b, actions, o, autoreset, hk);
-        else
-            CTR_LAUNCH_PAIR(k_step_pair, kc.mode, dim3(pair_grid(b.n)), shm, s, kc, b, actions, o, autoreset);
-    } else
-#endif
     if (her)
         CTR_LAUNCH(k_step_her, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
     else

@@ -39,6 +39,10 @@ class HerReplayBuffer(object):
             raise ValueError("goal_selection_strategy must be one of %s" % sorted(STRATEGIES))
         if int(slots) < 2:
             raise ValueError("slots must be >= 2 (one episode is always being recorded)")
+        if venv.obs_dtype != torch.float32:
+            # ctr_her_open / ctr_her_record / the fused recording read the env's observation
+            # rows as float32
+            raise ValueError("the HER feed records float32 observations: build the env with obs_dtype='float32'")
         self.venv = venv
         self.lib = venv.lib
         self.n_sampled_goal = int(n_sampled_goal)

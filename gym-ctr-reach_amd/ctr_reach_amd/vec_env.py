@@ -227,8 +227,6 @@ class CtrReachVecEnv(object):
         """Bind a device HER replay feed (ctr_reach_amd.her.HerReplayBuffer): every later reset /
         step records into it.  Call before reset()."""
         from .her import HerReplayBuffer
-        if self.obs_dtype != _torch().float32:
-            raise ValueError("the HER feed records float32 observations: use obs_dtype='float32'")
         return HerReplayBuffer(self, slots=slots, n_sampled_goal=n_sampled_goal,
                                goal_selection_strategy=goal_selection_strategy, seed=seed)
 
@@ -494,17 +492,28 @@ class CtrReachVecEnv(object):
         """Restore the batch state.  The reset pool is re-keyed to the restored reset numbers
         (queue dropped, next pool_depth resets requeued and refilled), the auto-reset miss
         counters are cleared, and a bound HER store drops its open episodes and opens new ones
-        from the restored state (the finished episodes it holds stay sampleable)."""
+        from the restored state (the finished episodes it holds stay sampleable).
+
+        Every key of ``state_dict()`` is required: a checkpoint without the observation (or any
+        other state buffer) would leave part of the live state from before the restore."""
+        missing = [k for k in self._STATE_KEYS + ("seed", "tol") if k not in sd]
+        if missing:
+            raise KeyError("checkpoint lacks %s (saved by an older build?)" % ", ".join(missing))
         for k in self._STATE_KEYS:
-            if k in sd:
-                getattr(self, k).copy_(sd[k])
+            getattr(self, k).copy_(sd[k])
         self.goal_tolerance.current_tol = sd["tol"]
         self.cfg.tol = float(sd["tol"])
         self.work.zero_()
         self._batch.work_parity = 0
+        seed_changed = int(sd["seed"]) != self.seed_value
         self.seed_value = int(sd["seed"])
         self.cfg.seed = self.seed_value & 0xFFFFFFFFFFFFFFFF
         if self.pool_depth:
+            if seed_changed:
+                # the ring's resets were drawn with the old seed: a slot whose reset number
+                # matches a restored epoch + j would otherwise be kept (requeue and refill only
+                # compare reset numbers)
+                self.pool_r.zero_()
             self._requeue_pool()
         if self._her is not None:
             self._her._open(None, None)
