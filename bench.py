@@ -18,8 +18,10 @@ Multi-GPU: ``python bench.py --gpus N`` launches N ranks itself (one process per
 anything touches a GPU); under ``torch.distributed.run`` the ranks come from the environment.
 Rank r owns the contiguous global env ids [r n, (r + 1) n) (weak scaling, no collective on the
 step itself).  With N > 1 every timed step also all-gathers the packed step outputs (16 B/env:
-tip, done | success | reward) over RCCL -- BASELINE configs[3] -- asynchronously on RCCL's
-stream while the next step runs; k_step writes the packed rows itself (pack_outputs).  A
+tip, done | success | reward) -- BASELINE configs[3] -- while the next step runs; k_step writes
+the packed rows itself (pack_outputs).  Default gather: the fused push (--gather-backend push,
+distributed.PushGather): k_step itself stores every env's row into every rank's IPC-mapped
+receive ring, with no extra launch; RCCL's kernels hold CUs the next step needs.  A
 barrier + device sync bracket the timed region and the time is the MAX over ranks.
 
 Also reported: the dominant kernel's roofline (algorithmic FP64 flops / its average launch
@@ -62,7 +64,8 @@ BYTES_RESET = 108
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="GPUs (ranks); default: WORLD_SIZE of a torch.distributed launcher, else 1")
     ap.add_argument("--steps", type=int, default=128, help="timed steps")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 5),
@@ -77,7 +80,14 @@ def parse():
     ap.add_argument("--refill-interval", type=int, default=None,
                     help="reset-pool refill interval (steps); default: the largest divisor of --steps <= 64")
     ap.add_argument("--gather", choices=("auto", "on", "off"), default="auto",
-                    help="RCCL all-gather of the packed step outputs in every timed step (auto: on when N > 1)")
+                    help="all-gather of the packed step outputs in every timed step (auto: on when N > 1)")
+    ap.add_argument("--gather-backend", choices=("push", "sdma", "rccl"), default="push",
+                    help="push: k_step itself stores every env's row into every rank's IPC-mapped receive ring "
+                         "(the fused push); sdma: copy-engine copies after the step (host-synchronous per copy in "
+                         "this runtime); rccl: all_gather_into_tensor over RCCL.  push / sdma fall back to rccl if "
+                         "the IPC setup fails")
+    ap.add_argument("--obs-dtype", choices=("float32", "float64"), default="float32",
+                    help="stored observation dtype (computed in float64 either way; float64 = the reference's)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group check only (CPU, gloo): no GPU, no env, no bench line")
     ap.add_argument("--no-stagger", action="store_true",
@@ -106,9 +116,24 @@ def self_launch(args):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll: if a rank dies (e.g. a communicator init failure) the others would block in a
+    # collective forever, so stop them and return the failed rank's code
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.05)
 
 
 def dist_init(args):
@@ -290,7 +315,7 @@ def main():
     systems = [int(s) for s in args.systems.split(",")]
     env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
                          integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"],
-                         select_systems=systems, refill_interval=R, pack_outputs=gather)
+                         select_systems=systems, refill_interval=R, pack_outputs=gather, obs_dtype=args.obs_dtype)
     env.reset()
     max_steps = env.max_steps_per_episode
     if not args.no_stagger:
@@ -299,7 +324,19 @@ def main():
         g.manual_seed(args.seed + 17 + rank)
         env.t.copy_(torch.randint(0, max_steps, (n,), generator=g, dtype=torch.int32))
     acts = make_actions(env, 8, args.seed + rank)
+    backend_used = None
+    fallback_note = None
     if gather:
+        backend_used = args.gather_backend
+        if backend_used in ("push", "sdma"):
+            try:
+                env.enable_gather(backend_used)
+            except Exception as ex:          # noqa: BLE001 -- reported in the line, RCCL measured instead
+                print("bench.py: %s gather setup failed (%s); using rccl" % (backend_used, ex), file=sys.stderr,
+                      flush=True)
+                backend_used = "rccl"
+                fallback_note = "%s setup failed: %s" % (args.gather_backend, str(ex)[:160])
+    if gather and backend_used == "rccl":
         # the env steps on a high-priority stream, RCCL's gather on its normal-priority one.  The
         # gather kernel (248-256 VGPRs, 37 KB LDS per workgroup) cannot share a SIMD with a k_step
         # wave (384 of the 512 registers), so whichever is dispatched first holds the CU: with the
@@ -311,12 +348,16 @@ def main():
     stream = torch.cuda.current_stream()
     works = [None, None]
 
+    pushg = gather and backend_used in ("push", "sdma")     # a PushGather (either engine)
+
     def one_step(i):
-        k = i & 1
-        if gather and works[k] is not None:
+        k = env._packed_k ^ 1        # the pack buffer this step writes
+        if gather and not pushg and works[k] is not None:
             works[k].wait()          # the gather that last read this pack buffer (stream-ordered, no host wait)
-        env.step_raw(acts[i % len(acts)])
-        if gather:
+        env.step_raw(acts[i % len(acts)])    # (push: the step itself stores its rows into every ring;
+        if pushg and backend_used == "sdma":  #  sdma: the step waits for the copies that read buffer k)
+            env.gather_outputs(backend=backend_used, async_op=True)
+        elif gather:
             _, works[k] = env.gather_outputs(async_op=True)
 
     # the window's bookkeeping (and the first barrier) once here: their first use loads kernels /
@@ -353,10 +394,33 @@ def main():
     for w in works:
         if w is not None:
             w.wait()
+    if pushg and backend_used == "sdma":
+        # every rank's pushes of the window: own copies done (sync), then the barrier after which
+        # every peer's copies into this rank's ring are done too (push: the rows are stored by the
+        # window's own k_step launches)
+        for ev in env._push_gather.done[0] + env._push_gather.done[1]:
+            torch.cuda.current_stream().wait_event(ev)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     gc.enable()
+    if pushg:
+        # the window's last gather, checked where it landed: this rank's slot holds every rank's
+        # rows of the last timed step (consumer wait, then a bit-exact compare with the gloo/RCCL
+        # copy of the same rows); outside the timed region
+        seq = env.gather_seq if backend_used == "push" else env.packed_seq
+        mine = env.packed_outputs().clone()
+        out = env._push_gather.wait(seq, torch.cuda.current_stream())
+        blocks = [torch.empty_like(mine) for _ in range(ws)]
+        if backend == "gloo":
+            hb = [b.cpu() for b in blocks]
+            dist.all_gather(hb, mine.cpu())
+            blocks = [b.to(dev) for b in hb]
+        else:
+            dist.all_gather(blocks, mine)
+        torch.cuda.synchronize()
+        gather_check = {"last_step_rows_equal": bool(torch.equal(out, torch.cat(blocks))),
+                        "wait_error": int(env._push_gather.err.item())}
     el = D.max_over_ranks(time.perf_counter() - t0, device=dev if backend in (None, "nccl") else "cpu")
     resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
     refills = env.refills - refills0
@@ -409,12 +473,19 @@ def main():
         "config": {"workload": (cfgd["text"] % n) + ", %s, n_substeps 10, tol 0.020, max 150 steps, "
                                                      "auto-reset" % ("system %d" % systems[0] if len(systems) == 1 else
                                                                      "systems %s drawn per reset" % args.systems)
-                   + (", RCCL all-gather of packed tip/reward/done every step" if gather else ""),
+                   + (", %s all-gather of packed tip/reward/done every step" %
+                      {"push": "fused-push", "sdma": "copy-engine (SDMA)", "rccl": "RCCL"}[backend_used]
+                      if gather else ""),
+                   "obs_dtype": args.obs_dtype,
                    "integrator": cfgd["integrator"], "model": cfgd["model"],
                    "rk4_steps_per_m": cfgd["rk4_steps_per_m"] if cfgd["integrator"] == "rk4" else None,
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
                    "process_group": {"backend": backend, "world_size": ws} if dist else None,
-                   "all_gather": {"bytes_per_env": 4 * D.PACK_WIDTH, "async": True} if gather else None,
+                   "all_gather": dict({"bytes_per_env": 4 * D.PACK_WIDTH, "async": True, "backend": backend_used},
+                                      **({"engine": env._push_gather.engine, "check": gather_check}
+                                         if pushg else {}),
+                                      **({"fallback": fallback_note} if fallback_note else {}))
+                   if gather else None,
                    "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,
                                   "autoreset": "pooled (no miss sweep)" if env.pool_depth >= env.refill_interval
                                   else "pooled + miss sweep"},

@@ -222,7 +222,6 @@ struct Trig {
     double c10, s10, c20, s20, c21, s21;   // cos/sin(alpha_i - alpha_j)
 };
 
-#ifndef CTR_TRIG_POLY
 // (sin, cos)(k pi/256) table for sincos_tab, one copy per workgroup in LDS; every kernel that
 // integrates calls trig_table_fill() before its first barrier.
 __shared__ double s_trig_tab[512][2];
@@ -231,9 +230,6 @@ __device__ __forceinline__ void trig_table_fill()
 {
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
 }
-#else
-__device__ __forceinline__ void trig_table_fill() {}
-#endif
 
 // CAREFUL: a wave-uniform ballot sends huge / non-finite angle differences (|d| >= 2^20) to the
 // exact out-of-line path.  The branch splits the stage code into basic blocks the scheduler
@@ -244,12 +240,7 @@ __device__ __forceinline__ Trig trig_of(const double al[3])
 {
     Trig t;
     const double d10 = al[1] - al[0], d20 = al[2] - al[0];
-#ifndef CTR_TRIG_POLY
     ctr_math::sincos_tab2(d10, d20, s_trig_tab, t.s10, t.c10, t.s20, t.c20);
-#else
-    ctr_math::sincos_fast(d10, t.s10, t.c10);
-    ctr_math::sincos_fast(d20, t.s20, t.c20);
-#endif
     if (CAREFUL &&
         __builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10) || ctr_math::sincos_needs_slow(d20)) != 0, 0)) {
         if (ctr_math::sincos_needs_slow(d10)) {
@@ -273,11 +264,7 @@ __device__ __forceinline__ Trig trig_of(const double al[3])
 // table's |x| < 2^20 range.
 __device__ __forceinline__ void sincos_lds(double x, double &s, double &c)
 {
-#ifndef CTR_TRIG_POLY
     ctr_math::sincos_tab(x, s_trig_tab, s, c);
-#else
-    ctr_math::sincos_fast(x, s, c);
-#endif
     if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(x)) != 0, 0) && ctr_math::sincos_needs_slow(x)) {
         const ctr_math::SinCos r = ctr_math::sincos_slow(x);
         s = r.s;
@@ -1104,11 +1091,7 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
 {
     const double beta[3] = {q[0], q[1], q[2]};
     double *end_lds = &s_seg_end[0][threadIdx.x];
-#ifdef CTR_GROUP_SORT_NETWORK
-    const Seg sg = seg_build(sy, beta, end_lds);
-#else
     const Seg sg = seg_build_group(sy, beta, end_lds, j);
-#endif
     const double ya[3] = {q[3], q[4], q[5]};
     const double yu[3] = {0.0, 0.0, 0.0};
     const Trig tconst = trig_of<CAREFUL>(ya);
@@ -1230,13 +1213,8 @@ __device__ __forceinline__ void obs_lane(const float q[6], const double dg[3], c
     }
     // the workgroup's LDS sincos table (<= 2 ulp, tests/test_math.py, like sincos_cw); angles
     // beyond its |x| < 2^20 range (never reached by bounded episodes) take the exact path
-#ifndef CTR_TRIG_POLY
     ctr_math::sincos_tab2(a[0], a[1], s_trig_tab, s[0], c[0], s[1], c[1]);
     ctr_math::sincos_tab(a[2], s_trig_tab, s[2], c[2]);
-#else
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) ctr_math::sincos_fast(a[i], s[i], c[i]);
-#endif
     if (__builtin_expect(__ballot(ctr_math::sincos_needs_slow(a[0]) || ctr_math::sincos_needs_slow(a[1]) ||
                                   ctr_math::sincos_needs_slow(a[2])) != 0, 0)) {
         #pragma unroll

@@ -166,6 +166,25 @@ __device__ __forceinline__ void wave_append(int32_t *counter, int32_t *items_bas
 __device__ __forceinline__ int32_t *miss_counter(const ctr_batch_t &b) { return b.work + (b.work_parity & 1); }
 __device__ __forceinline__ int32_t *miss_items(const ctr_batch_t &b) { return b.work + 2; }
 
+// The fused push gather (ctr_step_out_t.gather): env e's packed row into every rank's receive
+// slot (IPC-mapped peer memory; the descriptor's pointers are wave-uniform scalar loads).
+typedef unsigned int row16_t __attribute__((ext_vector_type(4)));   // one packed row
+
+__device__ __forceinline__ void gather_store_row(const ctr_gather_push_t *g, int64_t e, float4 row)
+{
+    const row16_t v = {__float_as_uint(row.x), __float_as_uint(row.y), __float_as_uint(row.z),
+                       __float_as_uint(row.w)};
+    const int W = g->world;
+    for (int k = 0; k < W; ++k) __builtin_nontemporal_store(v, static_cast<row16_t *>(g->dst[k]) + e);
+}
+
+// Lane k < world publishes seq into rank k's sequence word (release, system scope).
+__device__ __forceinline__ void gather_publish_lane(const ctr_gather_push_t *g, uint32_t seq)
+{
+    if ((int)threadIdx.x < g->world)
+        __hip_atomic_store(g->seqw[threadIdx.x], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Row e of an observation buffer: float32 [n][od] or, with cfg.obs_f64, float64 [n][od].
 __device__ __forceinline__ void write_obs(void *base, int64_t e, const double ob[14], bool multi, bool f64)
 {
@@ -398,12 +417,14 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
     o.error[e] = (float)d;
     uint32_t stat = st.status;
     if (o.nfev) o.nfev[e] = st.nfev;
-    if (o.packed) {
+    if (o.packed || o.gather) {
         // the gather row of this step (distributed.PACK_WIDTH, one 16-B store): the pre-reset tip,
         // so a done env reports where its episode ended, and done | success << 1 | (reward = -1)
         // << 2 (the sparse reward is -1 or 0, ctr_reach_env.py:169)
         const float fl = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0) | ((reward < 0.0f) ? 4 : 0));
-        *reinterpret_cast<float4 *>(o.packed + 4 * e) = make_float4((float)ag[0], (float)ag[1], (float)ag[2], fl);
+        const float4 row = make_float4((float)ag[0], (float)ag[1], (float)ag[2], fl);
+        if (o.packed) *reinterpret_cast<float4 *>(o.packed + 4 * e) = row;
+        if (o.gather) gather_store_row(o.gather, e, row);      // the fused push gather
     }
     // ctr_step_her: the transition goes into the env's HER episode before any auto-reset
     if (her) {
@@ -489,6 +510,12 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     const int j = (int)(gl % G);
     const bool in = e < b.n;                 // the lane works on a live env
     const bool live = in && j == 0;          // ... and is its lead lane (every per-env write)
+    // the step's sequence word after the packed rows (the copy-engine gather pushes it after them)
+    if (o.packed && o.packed_seq && blockIdx.x == 0 && threadIdx.x == 0)
+        *reinterpret_cast<uint4 *>(o.packed + 4 * b.n) = make_uint4(o.packed_seq, 0u, 0u, 0u);
+    // fused push gather: the previous gathered step's launch has completed, so its rows are in
+    // every rank's ring; publish its sequence word there
+    if (o.gather_prev && blockIdx.x == 0) gather_publish_lane(o.gather_prev, o.gather_prev_seq);
     StepFlags fl;
     if constexpr (GROUP) {
         // every lane of the wave takes part in the group's shuffles
@@ -1061,3 +1088,4 @@ int ctr_compute_reward(const double *achieved, const double *desired, int64_t n,
 }  // extern "C"
 
 #include "ctr_her.inc"
+#include "ctr_gather.inc"

@@ -42,20 +42,6 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
     r = fma(-n, 6.123233995736766e-17, r);
     r = fma(-n, -1.4973849048591698e-33, r);
     const double z = r * r;
-#ifdef CTR_SINCOS_HORNER
-    // sin kernel (|r| <= pi/4)
-    const double ps = 8.33333333332248946124e-03 +
-                      z * (-1.98412698298579493134e-04 +
-                           z * (2.75573137070700676789e-06 +
-                                z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
-    const double s = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
-    // cos kernel
-    const double pc = z * (4.16666666666666019037e-02 +
-                           z * (-1.38888888888741095749e-03 +
-                                z * (2.48015872894767294178e-05 +
-                                     z * (-2.75573143513906633035e-07 +
-                                          z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
-#else
     // Estrin evaluation of the same minimax kernels: dependency depth 3 instead of 5-6 (one
     // wave per SIMD exposes fp64 FMA latency)
     const double z2 = z * z;
@@ -67,7 +53,6 @@ CTR_HD void sincos_fast(double x, double &sv, double &cv)
     const double cb = fma(z, -2.75573143513906633035e-07, 2.48015872894767294178e-05);
     const double c3 = fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
     const double pc = z * fma(z2, fma(z2, c3, cb), ca);
-#endif
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double c = w + (((1.0 - w) - hz) + z * pc);

@@ -10,7 +10,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 10
+CTR_ABI_VERSION = 11
+CTR_IPC_HANDLE_BYTES = 64
+CTR_GATHER_MAX_RANKS = 16
 CTR_MAX_SYSTEMS = 8
 CTR_HER_SCAN_TILE = 1024
 CTR_INTEGRATOR_RK45_SCIPY = 0
@@ -104,7 +106,23 @@ class CtrStepOut(ctypes.Structure):
         ("status", _P),
         ("nfev", _P),
         ("packed", _P),
+        ("packed_seq", ctypes.c_uint32),
+        ("packed_pad", ctypes.c_uint32),
+        ("gather", _P),
+        ("gather_prev", _P),
+        ("gather_prev_seq", ctypes.c_uint32),
+        ("gather_pad", ctypes.c_uint32),
     ]
+
+
+class CtrGatherPush(ctypes.Structure):
+    _fields_ = [("src", _P), ("n", ctypes.c_int64), ("world", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("dst", _P * CTR_GATHER_MAX_RANKS), ("seqw", _P * CTR_GATHER_MAX_RANKS), ("ticket", _P)]
+
+
+class CtrCopy(ctypes.Structure):
+    _fields_ = [("dst", _P), ("src", _P), ("bytes", ctypes.c_int64), ("stream", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
 
 
 class CtrHer(ctypes.Structure):
@@ -136,7 +154,9 @@ class CtrHerBatch(ctypes.Structure):
 
 EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset",
             "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
-            "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her", "ctr_pool_requeue")
+            "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her", "ctr_pool_requeue",
+            "ctr_ipc_get_handle", "ctr_ipc_open", "ctr_ipc_close", "ctr_seqw_alloc", "ctr_seqw_free", "ctr_copy_list",
+            "ctr_gather_wait", "ctr_gather_push", "ctr_gather_publish")
 
 _lib = None
 
@@ -176,11 +196,26 @@ def load(path=None):
                                  ctypes.POINTER(CtrHerBatch), _P]
     L.ctr_step_her.argtypes = [ctypes.POINTER(CtrEnvConfig), ctypes.POINTER(CtrBatch), _P,
                                ctypes.POINTER(CtrStepOut), i32, ctypes.POINTER(CtrHer), _P]
-    for fn in ("ctr_fk", "ctr_set_action", "ctr_step", "ctr_reset", "ctr_pool_refill", "ctr_compute_reward",
-               "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
-               "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her", "ctr_pool_requeue"):
-        getattr(L, fn).restype = ctypes.c_int
-    if L.ctr_abi_version() != CTR_ABI_VERSION:
+    try:           # ABI 11 (an allowed older A/B build lacks them)
+        L.ctr_ipc_get_handle.argtypes = [_P, _P]
+        L.ctr_ipc_open.argtypes = [_P, ctypes.POINTER(_P)]
+        L.ctr_ipc_close.argtypes = [_P]
+        L.ctr_seqw_alloc.argtypes = [i64, ctypes.POINTER(_P)]
+        L.ctr_seqw_free.argtypes = [_P]
+        L.ctr_copy_list.argtypes = [ctypes.POINTER(CtrCopy), i32, ctypes.POINTER(_P), i32, _P, ctypes.POINTER(_P)]
+        L.ctr_gather_wait.argtypes = [_P, i32, ctypes.c_uint32, ctypes.c_uint32, _P, _P]
+        L.ctr_gather_push.argtypes = [ctypes.POINTER(CtrGatherPush), ctypes.c_uint32, i32, _P]
+        L.ctr_gather_publish.argtypes = [_P, ctypes.c_uint32, _P]
+    except AttributeError:
+        if L.ctr_abi_version() == CTR_ABI_VERSION:
+            raise
+    for fn in EXPORTED[2:]:
+        if hasattr(L, fn):
+            getattr(L, fn).restype = ctypes.c_int
+    # A/B timing of an older build (tools/experiments/build_rev.sh) may name its ABI version in
+    # CTR_REACH_AMD_ALLOW_ABI; only entry points both versions share may then be called
+    allowed = {CTR_ABI_VERSION, int(os.environ.get("CTR_REACH_AMD_ALLOW_ABI", CTR_ABI_VERSION))}
+    if L.ctr_abi_version() not in allowed:
         raise CtrError("ABI version mismatch: library %d, binding %d" % (L.ctr_abi_version(), CTR_ABI_VERSION))
     _lib = L
     return L

@@ -84,3 +84,264 @@ def max_over_ranks(value, device=None, group=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+# ---------------------------------------------------------------------------------------------
+# Push all-gather (configs[3] without RCCL's CU-holding kernels)
+#
+# RCCL's all-gather runs as kernels whose workgroups (248-256 VGPRs per lane) cannot share a SIMD
+# with a k_step wave, so the gather of step t holds CUs that step t + 1 needs (DESIGN.md section
+# 6).  PushGather moves the same bytes without them: every rank maps every rank's receive ring once
+# (IPC handles exchanged over the process group), and each step's rows go into slot `seq % depth`
+# of every ring, followed by the step's sequence word.  Engines:
+#   "fused"  k_step itself stores each env's row into every rank's slot (ctr_step_out_t.gather:
+#            8 extra 16-B stores per lane at the end of the step), and the NEXT k_step launch
+#            publishes the sequence words (its predecessor has completed, so the rows are
+#            performed); a consumer that waits before the next step publishes them itself
+#            (ctr_gather_publish).  No extra launch, no cross-stream dependency per step.
+#   "sdma"   ctr_copy_list after the step: copy-engine copies (no CU at all) of the packed rows;
+#            measured host-synchronous per copy in this runtime (~25 us each), so it cannot keep
+#            up with a step; kept selectable
+# (A standalone push kernel on a side stream, ctr_gather_push, overlaps the step but each step
+# then waits on a cross-stream event: ~10 us per hop, measured)
+# Layout of a receive ring: [depth][world][n][4] float32, so a slot is the rank-major =
+# global-id-ordered [world * n, 4] gather; sequence words [depth][world] uint32 (word [slot][r] =
+# the last step rank r published into that slot).  Ring and words are uncached device memory:
+# other GPUs write them, so this GPU's L2 must not serve stale lines.
+#
+# Reuse rule: slot s is rewritten by step seq + depth, so a consumer reads step seq before any
+# rank pushes step seq + depth (ctr_gather_wait flags a slot overwritten before it was consumed).
+
+class HipCopyOps(object):
+    """The device side of PushGather: libctr_reach_amd.so's IPC, uncached memory, descriptor,
+    publish, copy-list and wait entry points (include/ctr_reach_amd.h)."""
+
+    def __init__(self, device):
+        from . import _abi
+        self._abi = _abi
+        self.lib = _abi.load()
+        self.device = device
+        self._arrays = {}
+
+    def alloc_shared(self, nbytes):
+        import ctypes
+        p = ctypes.c_void_p()
+        self._abi.check(self.lib.ctr_seqw_alloc(int(nbytes), ctypes.byref(p)), "ctr_seqw_alloc")
+        return p.value
+
+    def free_shared(self, ptr):
+        self.lib.ctr_seqw_free(ptr)
+
+    def handle(self, ptr):
+        import ctypes
+        buf = ctypes.create_string_buffer(self._abi.CTR_IPC_HANDLE_BYTES)
+        self._abi.check(self.lib.ctr_ipc_get_handle(ptr, buf), "ctr_ipc_get_handle")
+        return buf.raw
+
+    def open(self, handle):
+        import ctypes
+        p = ctypes.c_void_p()
+        self._abi.check(self.lib.ctr_ipc_open(handle, ctypes.byref(p)), "ctr_ipc_open")
+        return p.value
+
+    def close(self, ptr):
+        self.lib.ctr_ipc_close(ptr)
+
+    def make_streams(self, k):
+        import torch
+        return [torch.cuda.Stream(device=self.device) for _ in range(k)]
+
+    def make_event(self):
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))      # created now, not lazily
+        return ev
+
+    def upload_descriptors(self, targets, n, ticket_ptr):
+        """Per-slot ctr_gather_push_t descriptors in device memory (the fused push reads them):
+        targets[slot] = [(row block dst, sequence word), ...] per rank.  Returns (keep-alive,
+        device pointer per slot)."""
+        import ctypes
+        import torch
+        size = ctypes.sizeof(self._abi.CtrGatherPush)
+        raw = bytearray()
+        for tg in targets:
+            g = self._abi.CtrGatherPush()
+            g.n, g.world, g.ticket = n, len(tg), ticket_ptr
+            for k, (dst, sw) in enumerate(tg):
+                g.dst[k], g.seqw[k] = dst, sw
+            raw += bytes(g)
+        dev = torch.frombuffer(raw, dtype=torch.uint8).to(self.device)
+        return dev, [dev.data_ptr() + i * size for i in range(len(targets))]
+
+    def publish(self, desc_ptr, seq, stream):
+        self._abi.check(self.lib.ctr_gather_publish(desc_ptr, seq & 0xFFFFFFFF, stream.cuda_stream),
+                        "ctr_gather_publish")
+
+    def native_plan(self, copies):
+        arr = (self._abi.CtrCopy * max(1, len(copies)))()
+        for i, (dst, src, nbytes, s) in enumerate(copies):
+            arr[i].dst, arr[i].src, arr[i].bytes, arr[i].stream = dst, src, nbytes, s
+        return arr, len(copies)
+
+    def copy_list(self, plan, streams, ready_event, done_events):
+        import ctypes
+        arr, n = plan["native"]
+        key = (id(streams), id(done_events))
+        if key not in self._arrays:      # the streams and per-parity event lists live as long as the gather
+            self._arrays[key] = ((ctypes.c_void_p * len(streams))(*[s.cuda_stream for s in streams]),
+                                 (ctypes.c_void_p * len(done_events))(*[e.cuda_event for e in done_events]))
+        sp, dp = self._arrays[key]
+        rc = self.lib.ctr_copy_list(arr, n, sp, len(streams), ready_event.cuda_event if ready_event else None, dp)
+        self._abi.check(rc, "ctr_copy_list")
+
+    def wait(self, seqw_ptr, n, seq, spin_limit, err, stream):
+        rc = self.lib.ctr_gather_wait(seqw_ptr, n, seq & 0xFFFFFFFF, spin_limit, err.data_ptr(), stream.cuda_stream)
+        self._abi.check(rc, "ctr_gather_wait")
+
+    def view(self, ptr, shape, dtype):
+        """A torch tensor over device memory this object allocated (CUDA array interface)."""
+        import torch
+        typestr = {torch.float32: "<f4", torch.int32: "<i4"}[dtype]
+
+        class _Iface(object):
+            __cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                        "version": 2, "strides": None, "stream": None}
+        t = torch.as_tensor(_Iface(), device=self.device)
+        assert t.data_ptr() == ptr and tuple(t.shape) == tuple(shape) and t.dtype == dtype
+        return t
+
+
+class PushWork(object):
+    """Handle of one push gather (the async_op result of gather_outputs(backend="push"/"sdma"))."""
+
+    def __init__(self, gather, seq):
+        self.gather, self.seq = gather, seq
+
+    def wait(self, stream=None):
+        """Enqueue the wait for every rank's block of this step on `stream` (default: current);
+        returns the gathered rows."""
+        import torch
+        return self.gather.wait(self.seq, stream if stream is not None else torch.cuda.current_stream())
+
+    def is_completed(self):
+        return False
+
+
+class PushGather(object):
+    """All-gather of every rank's packed step rows ([n, 4] float32: tip, done | success << 1 |
+    (reward = -1) << 2) by pushes into IPC-mapped receive rings (see the section comment).
+
+    fused engine (the env drives it around each ctr_step):
+      step_args(seq)           (descriptor of seq's slot, descriptor to publish, its seq) for
+                               ctr_step_out_t.gather / gather_prev / gather_prev_seq
+      stepped(seq)             the step launch with seq was enqueued (its words are pending)
+    sdma engine:
+      push(packed, seq, ready_event, parity)   copy-engine copies of packed ([n + 1, 4]: row n is
+                               the sequence row k_step writes with ctr_step_out_t.packed_seq)
+      wait_pushed(parity, stream)  before a step rewrites pack buffer `parity`
+    both:
+      wait(seq, stream)        enqueue the consumer wait for step seq (publishing it first if no
+                               later step did) and return the gathered [world * n, 4] rows
+    ``ops`` is the device backend (HipCopyOps; tests pass a CPU stand-in)."""
+
+    def __init__(self, n, group=None, depth=2, engine="fused", n_streams=None, device=None, ops=None,
+                 spin_limit=1 << 24):
+        import torch
+        import torch.distributed as dist
+        if engine not in ("fused", "sdma"):
+            raise ValueError("engine must be 'fused' or 'sdma'")
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.n, self.depth, self.engine = int(n), int(depth), engine
+        if self.depth < 1:
+            raise ValueError("depth must be >= 1")
+        if self.world > 16:
+            raise ValueError("at most 16 ranks (CTR_GATHER_MAX_RANKS)")
+        self.ops = ops if ops is not None else HipCopyOps(device)
+        self.spin_limit = int(spin_limit)
+        W, n4 = self.world, self.n * PACK_WIDTH * 4
+        self.block_bytes = n4
+        self.recv_ptr = self.ops.alloc_shared(self.depth * W * n4)
+        self.seqw_ptr = self.ops.alloc_shared(self.depth * W * 4 + 64)     # + this rank's push ticket
+        self.ticket_ptr = self.seqw_ptr + self.depth * W * 4
+        mine = (self.ops.handle(self.recv_ptr), self.ops.handle(self.seqw_ptr))
+        allh = [None] * W
+        dist.all_gather_object(allh, mine, group=group)
+        self.peer_recv = [self.recv_ptr if p == self.rank else self.ops.open(allh[p][0]) for p in range(W)]
+        self.peer_seqw = [self.seqw_ptr if p == self.rank else self.ops.open(allh[p][1]) for p in range(W)]
+        self.recv = self.ops.view(self.recv_ptr, (self.depth, W, self.n, PACK_WIDTH), torch.float32)
+        self.seqw = self.ops.view(self.seqw_ptr, (self.depth, W), torch.int32)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.pending = 0          # fused: the last pushed step whose words are not yet published
+        if engine == "fused":
+            self._desc_keep, self.desc = self.ops.upload_descriptors(
+                [self.targets(s) for s in range(self.depth)], self.n, self.ticket_ptr)
+            self.n_streams = 0
+        else:
+            # the copies to peer (rank + 1 + i) % world go on stream i % n_streams (different engines)
+            self.n_streams = max(1, min(int(n_streams or W), W))
+            self.streams = self.ops.make_streams(self.n_streams)
+            self.done = [[self.ops.make_event() for _ in range(self.n_streams)] for _ in range(2)]
+            self._plans = {}
+
+    def targets(self, slot):
+        """(row block destination, sequence word) in every rank for this rank's block of `slot`:
+        rank-major offsets, starting at the next rank (so the ranks write to different peers at a
+        time) and ending with this rank's own ring."""
+        W, r = self.world, self.rank
+        off = (slot * W + r) * self.block_bytes
+        woff = (slot * W + r) * 4
+        return [(self.peer_recv[(r + 1 + i) % W] + off, self.peer_seqw[(r + 1 + i) % W] + woff) for i in range(W)]
+
+    # ---- fused engine
+    def step_args(self, seq):
+        prev = self.pending
+        return self.desc[seq % self.depth], (self.desc[prev % self.depth] if prev else None), prev
+
+    def stepped(self, seq):
+        self.pending = seq
+
+    # ---- sdma engine
+    def plan(self, src_ptr, slot):
+        key = (src_ptr, slot)
+        if key not in self._plans:
+            copies = []
+            for i, (dst, sw) in enumerate(self.targets(slot)):
+                s = i % self.n_streams
+                copies.append((dst, src_ptr, self.block_bytes, s))
+                copies.append((sw, src_ptr + self.block_bytes, 4, s))
+            self._plans[key] = {"copies": copies, "native": self.ops.native_plan(copies)}
+        return self._plans[key]
+
+    def push(self, packed, seq, ready_event, parity=None):
+        """packed: [n + 1, 4] float32 whose row n holds seq (k_step with packed_seq = seq)."""
+        if self.engine != "sdma":
+            raise RuntimeError("push() is the sdma engine's; the fused push runs inside the step")
+        if packed.shape[0] != self.n + 1:
+            raise ValueError("packed must hold n + 1 rows (the sequence row)")
+        parity = (seq & 1) if parity is None else parity
+        self.ops.copy_list(self.plan(packed.data_ptr(), seq % self.depth), self.streams, ready_event,
+                           self.done[parity])
+
+    def wait_pushed(self, parity, stream):
+        if self.engine == "sdma":
+            for ev in self.done[parity & 1]:
+                stream.wait_event(ev)
+
+    # ---- consumer
+    def wait(self, seq, stream):
+        slot = seq % self.depth
+        if self.engine == "fused" and self.pending == seq:
+            self.ops.publish(self.desc[slot], seq, stream)     # no later step has published it
+            self.pending = 0
+        self.ops.wait(self.seqw_ptr + slot * self.world * 4, self.world, seq, self.spin_limit, self.err, stream)
+        return self.recv[slot].reshape(self.world * self.n, PACK_WIDTH)
+
+    def close(self):
+        for p in range(self.world):
+            if p != self.rank:
+                self.ops.close(self.peer_recv[p])
+                self.ops.close(self.peer_seqw[p])
+        self.ops.free_shared(self.recv_ptr)
+        self.ops.free_shared(self.seqw_ptr)

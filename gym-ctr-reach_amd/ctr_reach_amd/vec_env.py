@@ -34,6 +34,11 @@ def _torch():
     return torch
 
 
+def _current_stream(stream, device):
+    import torch
+    return stream if stream is not None else torch.cuda.current_stream(device)
+
+
 def joint_spaces(systems, constrain_alpha):
     """Obs.get_joint_space (obs.py:50-76): per-system (joint_space, joint_sample_space)."""
     js, jss = [], []
@@ -159,8 +164,12 @@ class CtrReachVecEnv(object):
         # pack_outputs: k_step also writes each step's gather row ([n, 4] f32, distributed.PACK_WIDTH)
         # into one of two alternating buffers, so gather_outputs() needs no packing launch and one
         # gather may stay in flight while the next step writes the other buffer
-        self.packed_bufs = [torch.zeros((n, D.PACK_WIDTH), dtype=f32, device=dev) for _ in range(2)] if pack_outputs else None
+        # (row n: the step's sequence word, for the copy-engine gather; see gather_outputs)
+        self.packed_bufs = [torch.zeros((n + 1, D.PACK_WIDTH), dtype=f32, device=dev) for _ in range(2)] if pack_outputs else None
         self._packed_k = 0
+        self.packed_seq = 0       # steps that wrote packed rows (the sequence word of the last one)
+        self._push_gather = None  # distributed.PushGather (enable_gather)
+        self.gather_seq = 0       # fused push: the last step pushed
         self.refills = 0          # ctr_pool_refill launches so far (bench accounting)
         self.sweeps = 0           # steps that launched the auto-reset miss sweep (CTR_AUTORESET_SWEEP)
         # reset pool: resets are a pure function of (seed, env id, reset number), so they are
@@ -325,6 +334,18 @@ class CtrReachVecEnv(object):
         if pb is not None:                     # this step writes the buffer the last gather did not
             self._packed_k ^= 1
             self._out.packed = pb[self._packed_k].data_ptr()
+            # never 0 (no sequence row) and parity-preserving at the uint32 wrap (done events by parity)
+            self.packed_seq = self.packed_seq + 1 if self.packed_seq < 0xFFFFFFFF else 2
+            self._out.packed_seq = self.packed_seq
+            if self._push_gather is not None:    # the copy engines have read this buffer's last rows
+                self._push_gather.wait_pushed(self._packed_k, _current_stream(stream, self.device))
+        g = self._push_gather
+        fused = g is not None and g.engine == "fused"
+        if fused:                              # this step also stores its rows into every rank's ring
+            self.gather_seq = self.gather_seq + 1 if self.gather_seq < 0xFFFFFFFF else 1
+            cur, prev, prev_seq = g.step_args(self.gather_seq)
+            o = self._out
+            o.gather, o.gather_prev, o.gather_prev_seq = cur, prev, prev_seq
         mode = _abi.AUTORESET_OFF
         if self.autoreset:
             # no done env can miss its pooled reset while at most pool_depth steps have run since
@@ -340,6 +361,10 @@ class CtrReachVecEnv(object):
             rc = self.lib.ctr_step_her(self.cfg, self._batch, _abi.ptr(actions), self._out, mode, her._h, sp)
         else:
             rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, mode, sp)
+        if fused:
+            o.gather = o.gather_prev = None    # only this launch pushes (other ctr_step users of _out do not)
+            if rc == 0:
+                g.stepped(self.gather_seq)
         if rc:
             _abi.check(rc, "ctr_step")
         if her is not None and not her.fused:  # ctr_her_record from the step's outputs
@@ -447,18 +472,63 @@ class CtrReachVecEnv(object):
         out["table"] = table
         return out
 
-    def gather_outputs(self, group=None, async_op=False):
+    def enable_gather(self, backend="push", group=None, depth=2):
+        """Set up the push all-gather (collective: every rank calls it).  "push": every later
+        step also stores its packed rows into every rank's receive ring (the fused push; no
+        extra launch); "sdma": gather_outputs(backend="sdma") copies them with the copy engines
+        (needs pack_outputs=True).  Returns the distributed.PushGather."""
+        if self._push_gather is not None:
+            raise RuntimeError("the gather is already enabled")
+        if backend == "sdma" and self.packed_bufs is None:
+            raise RuntimeError("the sdma gather needs CtrReachVecEnv(..., pack_outputs=True)")
+        if backend not in ("push", "sdma"):
+            raise ValueError("backend must be 'push' or 'sdma'")
+        self._push_gather = D.PushGather(self.num_envs, group=group, depth=depth, device=self.device,
+                                         engine="fused" if backend == "push" else "sdma")
+        return self._push_gather
+
+    def gather_outputs(self, group=None, async_op=False, backend="rccl", depth=2):
         """Optional collective for a single-process trainer: every rank's last-step (tip, reward,
-        done, success) packed to 16 B/env and all-gathered over RCCL -> [world * n, 4] float32
-        in global-id order.  Not used on the stepping path.  async_op=True returns (out, work)
-        and lets the next step() run while the gather is in flight (RCCL's stream); the pack
-        buffers alternate, so one gather may be outstanding per env.
+        done, success) packed to 16 B/env and all-gathered -> [world * n, 4] float32 in global-id
+        order.  Not used on the stepping path.  async_op=True returns (out, work) and lets the
+        next step() run while the gather is in flight; the pack buffers alternate, so one gather
+        may be outstanding per env.
+
+        backend "rccl": all_gather_into_tensor over RCCL (its own stream).  backend "push" (after
+        enable_gather("push"): the last step already stored its rows into every rank's ring) or
+        "sdma" (copy engines, needs pack_outputs=True; set up on first use, collectively): this
+        rank's rows land in every rank's IPC-mapped receive ring (distributed.PushGather); ``out``
+        is slot (step % depth) of this rank's ring, valid after ``work.wait()`` (which enqueues
+        the wait for every rank's block on the current stream) until step + depth is gathered.
 
         With ``pack_outputs=True`` the step kernel itself wrote the packed rows (no packing
         launch); otherwise they are packed here from the step's outputs."""
         import torch
+        if backend in ("push", "sdma"):
+            if self._push_gather is None:
+                if backend == "push":
+                    raise RuntimeError("the fused push gather is part of the step: call enable_gather('push') "
+                                       "before stepping")
+                self.enable_gather("sdma", group=group, depth=depth)
+            g = self._push_gather
+            if (g.engine == "fused") != (backend == "push"):
+                raise RuntimeError("this env gathers with the %s engine" % g.engine)
+            if g.engine == "fused":
+                seq = self.gather_seq              # pushed by the last step itself
+            else:
+                ready = self._gather_ready = getattr(self, "_gather_ready", None) or torch.cuda.Event()
+                ready.record(torch.cuda.current_stream(self.device))
+                seq = self.packed_seq
+                g.push(self.packed_bufs[self._packed_k], seq, ready, parity=self._packed_k)
+            work = D.PushWork(g, seq)
+            if async_op:
+                return g.recv[seq % g.depth].reshape(-1, D.PACK_WIDTH), work
+            return work.wait()
+        if backend != "rccl":
+            raise ValueError("backend must be 'rccl', 'push' or 'sdma'")
         if self.packed_bufs is not None:
-            return D.all_gather_outputs(self.packed_bufs[self._packed_k], group=group, async_op=async_op)
+            return D.all_gather_outputs(self.packed_bufs[self._packed_k][:self.num_envs], group=group,
+                                        async_op=async_op)
         d = self.done.bool()
         tip = torch.where(d[:, None], self.terminal_achieved, self.achieved_goal) if self.autoreset else self.achieved_goal
         bufs = getattr(self, "_packed", None) or [None, None]
@@ -471,7 +541,7 @@ class CtrReachVecEnv(object):
         """The last step's packed rows ([n, 4] float32, see gather_outputs); needs pack_outputs=True."""
         if self.packed_bufs is None:
             raise RuntimeError("packed_outputs() needs CtrReachVecEnv(..., pack_outputs=True)")
-        return self.packed_bufs[self._packed_k]
+        return self.packed_bufs[self._packed_k][:self.num_envs]
 
     def update_goal_tolerance(self, timestep):
         self.goal_tolerance.update(timestep)

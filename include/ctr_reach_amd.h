@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 10
+#define CTR_ABI_VERSION 11
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -164,6 +164,8 @@ typedef struct ctr_batch_t {
     int64_t   refill_cap;
 } ctr_batch_t;
 
+typedef struct ctr_gather_push_t ctr_gather_push_t;   /* defined with the push gather below */
+
 /* Per-step outputs (device). obs_dim = 13, or 14 when n_systems > 1 (obs.py:153-156). */
 typedef struct ctr_step_out_t {
     void     *obs;               /* [n][obs_dim]   observation after the step (after auto-reset);
@@ -183,6 +185,22 @@ typedef struct ctr_step_out_t {
                                     done | success << 1 | (reward == -1) << 2 as a float (the
                                     reward is -1 or 0).  Written by k_step itself, so gathering
                                     costs no packing launch.                                      */
+    uint32_t  packed_seq;        /* != 0 (with packed): k_step also writes row n of packed as
+                                    (packed_seq, 0, 0, 0) as uint32 bits, the step's sequence word
+                                    that ctr_copy_list pushes after the rows (packed then holds
+                                    n + 1 rows).  0: row n is not touched.                        */
+    uint32_t  packed_pad;
+    const ctr_gather_push_t *gather;      /* device or NULL: the fused push gather -- k_step also
+                                             stores each env's packed row (as in `packed`) into
+                                             every rank's receive slot, gather->dst[p] + e for
+                                             p < gather->world (IPC-mapped peer memory)          */
+    const ctr_gather_push_t *gather_prev; /* device or NULL: the first lanes of k_step publish
+                                             gather_prev_seq to every gather_prev->seqw[p]
+                                             (release, system scope) -- the previous gathered
+                                             step, whose launch has completed (so its row stores
+                                             are performed) before this one starts               */
+    uint32_t  gather_prev_seq;
+    uint32_t  gather_pad;
 } ctr_step_out_t;
 
 /* ---------------------------------------------------------------------------------------
@@ -347,6 +365,85 @@ int ctr_pool_requeue(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void
  * re-sampled Tube inputs; U_x is in sys_out) may each be NULL.  (device) */
 int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr_system_t *sys_out,
                       ctr_tube_raw_t *raw_out, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Push all-gather of the packed step rows (BASELINE configs[3]: a single-process trainer that
+ * wants every GPU's tip / reward / done; no reference counterpart -- the reference runs one env
+ * per process).  Each rank pushes its [n][4] block of packed rows into every rank's receive ring
+ * (IPC-mapped), then the block's sequence word into the receiver's sequence words (uncached device
+ * memory).  Engines: the fused push (ctr_step_out_t.gather: k_step itself stores every env's row
+ * into every rank's slot, and the next launch publishes the sequence words), ctr_gather_push (the
+ * same stores as a standalone slim kernel), and ctr_copy_list, copy-engine copies (no CU at all,
+ * but host-synchronous per copy in this runtime; the sequence word then comes from row n of the
+ * packed rows, written by k_step: ctr_step_out_t.packed_seq).  RCCL's collective kernels, the
+ * other option, cannot share a SIMD with k_step, so they hold CUs the next step needs.
+ * A consumer waits for a step with ctr_gather_wait.  The host side
+ * (ctr_reach_amd.distributed.PushGather) plans the destinations: receive ring
+ * [depth][world][n][4] float32 (rank-major = global env id order within a slot), sequence words
+ * [depth][world] uint32.
+ * ------------------------------------------------------------------------------------- */
+#define CTR_IPC_HANDLE_BYTES 64
+#define CTR_GATHER_MAX_RANKS 16
+
+/* One rank's push of its block: the host struct of ctr_gather_push, and (in device memory) the
+ * per-slot descriptor of the fused push (ctr_step_out_t.gather; src, n and ticket unused there). */
+struct ctr_gather_push_t {
+    const void *src;                          /* [n][4] float32 packed rows (16-B aligned)     */
+    int64_t     n;
+    int32_t     world;
+    int32_t     pad;
+    void       *dst[CTR_GATHER_MAX_RANKS];    /* rank p's copy of this block: its receive ring
+                                                 slot + rank * n rows (IPC-mapped)           */
+    uint32_t   *seqw[CTR_GATHER_MAX_RANKS];   /* this block's sequence word in rank p's memory  */
+    uint32_t   *ticket;                       /* this rank's device word, zero-initialised (the
+                                                 kernel leaves it zero)                      */
+};
+
+/* Enqueue the push kernel: the n rows to every dst[p] (p < world), then seq to every seqw[p]
+ * (after all rows, release at system scope).  workgroups: grid size (e.g. 128); its waves use
+ * ~20 VGPRs and no LDS, so they share SIMDs with k_step waves. */
+int ctr_gather_push(const ctr_gather_push_t *g, uint32_t seq, int32_t workgroups, void *stream);
+
+/* Publish seq to every g_dev->seqw[p] (release, system scope) after the work already on
+ * `stream`: the fused push's explicit publication of its last step (k_step publishes the previous
+ * step itself, ctr_step_out_t.gather_prev).  g_dev: device descriptor.  One wave. */
+int ctr_gather_publish(const ctr_gather_push_t *g_dev, uint32_t seq, void *stream);
+
+/* hipIpcGetMemHandle of a device allocation (handle: CTR_IPC_HANDLE_BYTES bytes, host). */
+int ctr_ipc_get_handle(const void *dev_ptr, void *handle);
+/* Map another process's allocation (hipIpcOpenMemHandle, peer access enabled lazily). */
+int ctr_ipc_open(const void *handle, void **dev_ptr);
+int ctr_ipc_close(void *dev_ptr);
+
+/* Uncached device memory for sequence words (zeroed; synchronous).  The only entry points that
+ * allocate: the words are written by other GPUs' copy engines and polled by ctr_gather_wait,
+ * so they must not sit in this GPU's L2. */
+int ctr_seqw_alloc(int64_t bytes, void **dev_ptr);
+int ctr_seqw_free(void *dev_ptr);
+
+/* One copy of a copy list. */
+typedef struct ctr_copy_t {
+    void       *dst;
+    const void *src;
+    int64_t     bytes;
+    int32_t     stream;      /* index into the streams of ctr_copy_list */
+    int32_t     pad;
+} ctr_copy_t;
+
+/* Enqueue copy-engine copies (hipMemcpyDeviceToDeviceNoCU): every stream first waits for
+ * ready_event (NULL: no wait), then runs its copies in list order, then records
+ * done_events[s] (NULL array or entry: none).  Copies on one stream are ordered, so a sequence
+ * word listed after its block lands after it. */
+int ctr_copy_list(const ctr_copy_t *copies, int32_t n_copies, void *const *streams, int32_t n_streams,
+                  void *ready_event, void *const *done_events);
+
+/* Consumer side: enqueue on `stream` a one-wave kernel that waits until seqw[i] reaches seq for
+ * every i < n (wrap-aware uint32 compare; seqw is uncached, polled at system scope), then
+ * returns.  err (device, uint32) gets bit 1 if spin_limit polls pass first (the kernel then
+ * returns anyway: no unbounded wait) and bit 2 if a word is already past seq (the slot was
+ * overwritten by a later step before it was consumed). */
+int ctr_gather_wait(const uint32_t *seqw, int32_t n, uint32_t seq, uint32_t spin_limit, uint32_t *err,
+                    void *stream);
 
 /* Batched compute_reward over leading dims: ag, dg [n][3] f64 -> reward [n] f32 in {-1, 0}. */
 int ctr_compute_reward(const double *achieved, const double *desired, int64_t n, double tol,

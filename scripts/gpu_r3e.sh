@@ -1,0 +1,19 @@
+# fused push gather: tests, interference, k_step A/B vs round 2, rehearsal benches
+set -o pipefail
+mkdir -p gpurun_out
+run() {   # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"; tail -${TAILN:-6} "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "abnormal exit, stopping"; exit $rc; fi
+}
+L=$PWD/gym-ctr-reach_amd/ctr_reach_amd/lib
+TAILN=8 run pytest_gather 300 python -u -m pytest tests/test_gpu_gather.py tests/test_gpu_rccl.py -x -v --timeout 120 --timeout-method thread
+run interf_fused8 240 python tools/gather_interference.py fused 8
+for v in libctr_reach_amd.so libab_r2.so libctr_reach_amd.so libab_r2.so; do
+  CTR_REACH_AMD_ALLOW_ABI=10 CTR_REACH_AMD_LIB=$L/$v run ab_$v 120 python tools/time_step_modes.py
+done
+run bench_n2_push 300 env CTR_BENCH_BACKEND=gloo CTR_BENCH_SAME_DEVICE=1 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline
+run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
+TAILN=4 run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread

@@ -29,6 +29,8 @@ Outputs (all seeded, deterministic):
                   reproduces them to 1e-12
   systems.json    the registration tube tables (ctr_reach_envs/__init__.py:7-70)
   sampler.npz     Obs.sample_goal draws per system (joints f32[4,n,6], candidates tried i32[4,n])
+  eval_info.npz   evaluation=True env.step() info dicts over short episodes from the reference's
+                  own reset() (select_systems [1, 3])
 
 Usage:  python tests/golden/make_golden.py  [--quick]
 """
@@ -428,6 +430,53 @@ def gen_sampler(CtrReachEnv, kwargs, per_sys):
     np.savez_compressed(os.path.join(OUT, "sampler.npz"), joints=np.array(J, np.float32), tries=np.array(T, np.int32))
 
 
+def gen_eval(CtrReachEnv, kwargs, episodes, steps):
+    """env.step() with evaluation=True (ctr_reach_env.py:144-153): the info dict the reference's
+    evaluation runs record (errors_pos, q_desired, q_achieved, q_starting, starting_position,
+    system_idx, ...), over short episodes.  select_systems [1, 3], so system_idx (the
+    registration index) differs from the episode's system (an index into select_systems).
+    Each episode starts from the reference's own reset() (np.random seeded per episode)."""
+    env = make_env(CtrReachEnv, kwargs, select_systems=[1, 3], evaluation=True, constrain_alpha=False)
+    alim = env.action_space.high
+    rng = np.random.default_rng(2024)
+    keys_vec = ("achieved_goal", "desired_goal", "starting_position", "q_desired", "q_achieved", "q_starting")
+    keys_sc = ("is_success", "errors_pos", "errors_orient", "system_idx", "position_tolerance",
+               "orientation_tolerance")
+    rows = {k: [] for k in keys_vec + keys_sc + ("episode", "t", "action", "reward", "done", "observation",
+                                                 "tol")}
+    resets = {k: [] for k in ("system", "desired_joints", "desired_goal", "starting_joints", "starting_position",
+                              "observation")}
+    for ep in range(episodes):
+        np.random.seed(500 + ep)
+        tol = float(rng.choice([0.02, 0.005]))
+        env.goal_tolerance.current_tol = tol
+        obs0 = env.reset()
+        resets["system"].append(int(env.system))
+        resets["desired_joints"].append(np.asarray(env.desired_joints, np.float32))
+        resets["desired_goal"].append(np.asarray(env.desired_goal, np.float64))
+        resets["starting_joints"].append(np.asarray(env.starting_joints, np.float32))
+        resets["starting_position"].append(np.asarray(env.starting_position, np.float64))
+        resets["observation"].append(np.asarray(obs0["observation"], np.float64))
+        for t in range(steps):
+            a = (rng.uniform(-1, 1, 6) * alim).astype(np.float32)
+            obs, reward, done, info = env.step(a)
+            assert set(info) == set(keys_vec + keys_sc)
+            for k in keys_vec:
+                rows[k].append(np.asarray(info[k], np.float64))
+            for k in keys_sc:
+                rows[k].append(float(info[k]))
+            rows["episode"].append(ep); rows["t"].append(t); rows["action"].append(a)
+            rows["reward"].append(float(reward)); rows["done"].append(bool(done)); rows["tol"].append(tol)
+            rows["observation"].append(np.asarray(obs["observation"], np.float64))
+            if done:
+                break
+    out = {k: np.array(v) for k, v in rows.items()}
+    out.update({"reset_" + k: np.array(v) for k, v in resets.items()})
+    out["select_systems"] = np.array([1, 3], np.int32)
+    np.savez_compressed(os.path.join(OUT, "eval_info.npz"), **out)
+    print("eval_info", episodes, "episodes", len(out["t"]), "steps")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -441,6 +490,8 @@ def main():
             gen_backbone(CtrReachEnv, kwargs, 4 if args.quick else 16)
         if "sampler" in args.only:
             gen_sampler(CtrReachEnv, kwargs, 400 if args.quick else 4000)
+        if "eval" in args.only:
+            gen_eval(CtrReachEnv, kwargs, 4 if args.quick else 24, 12)
         return
     sysj = {}
     for s in range(4):
@@ -459,6 +510,7 @@ def main():
     gen_jacobian(CtrReachEnv, kwargs, 4 if args.quick else 32)
     gen_backbone(CtrReachEnv, kwargs, 4 if args.quick else 16)
     gen_sampler(CtrReachEnv, kwargs, 400 if args.quick else 4000)
+    gen_eval(CtrReachEnv, kwargs, 4 if args.quick else 24, 12)
 
 
 if __name__ == "__main__":

@@ -141,3 +141,162 @@ def test_refill_interval_tiles_the_window():
     for k in range(1, 300):
         ri = bench.refill_interval_for(k)
         assert k % ri == 0 and 1 <= ri <= 64
+
+
+class _ShmCopyOps(object):
+    """CPU stand-in for distributed.HipCopyOps: "device memory" is a /dev/shm mapping, an IPC
+    handle is its path, a copy is a memmove and the wait polls the sequence words.  It runs
+    PushGather's own planning (handle exchange, rank-major offsets, sequence words)."""
+
+    def __init__(self):
+        self.maps = {}
+
+    def _map(self, path, nbytes=None):
+        import ctypes
+        import mmap
+        fd = os.open(path, os.O_RDWR | (os.O_CREAT if nbytes else 0))
+        try:
+            if nbytes:
+                os.ftruncate(fd, nbytes)
+            mm = mmap.mmap(fd, 0)
+        finally:
+            os.close(fd)
+        addr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+        self.maps[addr] = (path, mm)
+        return addr
+
+    def alloc_shared(self, nbytes):
+        return self._map("/dev/shm/ctr_ce_test_%d_%d" % (os.getpid(), len(self.maps)), nbytes)
+
+    def free_shared(self, ptr):
+        os.unlink(self.maps[ptr][0])
+
+    def handle(self, ptr):
+        return self.maps[ptr][0].encode()
+
+    def open(self, handle):
+        return self._map(handle.decode())
+
+    def close(self, ptr):
+        pass
+
+    def make_streams(self, k):
+        return [None] * k
+
+    def make_event(self):
+        return None
+
+    def native_plan(self, copies):
+        return None
+
+    def upload_descriptors(self, targets, n, ticket_ptr):
+        return None, [list(t) for t in targets]
+
+    def publish(self, desc, seq, stream):
+        import ctypes
+        for dst, sw in desc:
+            ctypes.c_uint32.from_address(sw).value = seq
+
+    def fused_step_stores(self, desc, rows):
+        """What k_step does with ctr_step_out_t.gather: every env's row into every target."""
+        import ctypes
+        for dst, sw in desc:
+            ctypes.memmove(dst, rows.data_ptr(), rows.numel() * 4)
+
+    def copy_list(self, plan, streams, ready_event, done_events):
+        import ctypes
+        for dst, src, nbytes, s in plan["copies"]:
+            assert 0 <= s < len(streams)
+            ctypes.memmove(dst, src, nbytes)
+
+    def wait(self, seqw_ptr, n, seq, spin_limit, err, stream):
+        import ctypes
+        import time
+        words = (ctypes.c_uint32 * n).from_address(seqw_ptr)
+        for _ in range(spin_limit):
+            if all(((w - seq) & 0xFFFFFFFF) < 0x80000000 for w in words):
+                break
+            time.sleep(0.001)
+        else:
+            err[0] |= 1
+            return
+        if any(w != seq for w in words):
+            err[0] |= 2
+
+    def view(self, ptr, shape, dtype):
+        import ctypes
+        nbytes = int(np.prod(shape)) * 4
+        buf = (ctypes.c_char * nbytes).from_address(ptr)
+        return torch.frombuffer(buf, dtype=dtype).reshape(shape)
+
+
+def _ce_worker(rank, world, port, n, engine, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = None
+    try:
+        from ctr_reach_amd import distributed as D
+        ops = _ShmCopyOps()
+        g = D.PushGather(n, depth=3, engine=engine, n_streams=2, ops=ops, spin_limit=5000)
+
+        def step(seq, packed):
+            if engine == "sdma":
+                g.push(packed, seq, None)
+            else:                      # the env's fused step: rows now, words by the next step
+                cur, prev, prev_seq = g.step_args(seq)
+                if prev is not None:
+                    ops.publish(prev, prev_seq, None)
+                ops.fused_step_stores(cur, packed[:n])
+                g.stepped(seq)
+        got = []
+        for seq in range(1, 6):
+            # this rank's packed block of step seq (+ the sequence row k_step writes)
+            packed = torch.zeros((n + 1, D.PACK_WIDTH), dtype=torch.float32)
+            packed[:n] = torch.arange(n * D.PACK_WIDTH, dtype=torch.float32).reshape(n, -1) + 1000 * rank + 1e5 * seq
+            packed[n, 0] = torch.tensor([seq], dtype=torch.int32).view(torch.float32)
+            step(seq, packed)
+            dist.barrier()
+            got.append(g.wait(seq, None).clone())     # (fused: publishes seq itself, no later step yet)
+            assert int(g.err[0]) == 0
+            dist.barrier()
+        # a slot overwritten before it was consumed is flagged: step 6 reuses step 3's slot
+        packed[n, 0] = torch.tensor([6], dtype=torch.int32).view(torch.float32)
+        step(6, packed)
+        if engine == "fused":
+            ops.publish(g.step_args(7)[1], 6, None)    # what step 7's launch would publish
+        dist.barrier()
+        g.wait(3, None)
+        overrun = int(g.err[0])
+        if rank == 0:
+            q.put((torch.stack(got).numpy(), g.seqw.numpy().copy(), overrun))
+        dist.barrier()
+    finally:
+        if g is not None:
+            g.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("engine", ["fused", "sdma"])
+def test_push_gather_exchange_and_layout(engine):
+    """PushGather on 3 gloo ranks with a CPU stand-in of the device side: the IPC handle
+    exchange, every rank's block at its rank-major offset of every receive slot (slot = step %
+    depth), the sequence words, and the overrun flag of a slot rewritten before it was read."""
+    world, n = 3, 16
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ce_worker, args=(r, world, port, n, engine, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, seqw, overrun = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    base = np.arange(n * 4, dtype=np.float32).reshape(n, 4)
+    for i, seq in enumerate(range(1, 6)):
+        want = np.concatenate([base + 1000 * r + 1e5 * seq for r in range(world)])
+        np.testing.assert_array_equal(got[i], want)
+    # depth 3: slot 0 last held step 6 (overrun test), slot 1 step 4, slot 2 step 5
+    np.testing.assert_array_equal(seqw, np.array([[6] * world, [4] * world, [5] * world]))
+    assert overrun == 2
