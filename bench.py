@@ -81,11 +81,12 @@ def parse():
                     help="reset-pool refill interval (steps); default: the largest divisor of --steps <= 64")
     ap.add_argument("--gather", choices=("auto", "on", "off"), default="auto",
                     help="all-gather of the packed step outputs in every timed step (auto: on when N > 1)")
-    ap.add_argument("--gather-backend", choices=("push", "sdma", "rccl"), default="push",
+    ap.add_argument("--gather-backend", choices=("auto", "push", "sdma", "rccl"), default="auto",
                     help="push: k_step itself stores every env's row into every rank's IPC-mapped receive ring "
                          "(the fused push); sdma: copy-engine copies after the step (host-synchronous per copy in "
-                         "this runtime); rccl: all_gather_into_tensor over RCCL.  push / sdma fall back to rccl if "
-                         "the IPC setup fails")
+                         "this runtime); rccl: all_gather_into_tensor over RCCL; auto: time push and rccl on 2 "
+                         "refill periods each (untimed) and run the window with the faster.  push / sdma / auto fall "
+                         "back to rccl if the IPC setup fails")
     ap.add_argument("--obs-dtype", choices=("float32", "float64"), default="float32",
                     help="stored observation dtype (computed in float64 either way; float64 = the reference's)")
     ap.add_argument("--dry-run", action="store_true",
@@ -326,39 +327,55 @@ def main():
     acts = make_actions(env, 8, args.seed + rank)
     backend_used = None
     fallback_note = None
+    calibration = None
     if gather:
         backend_used = args.gather_backend
-        if backend_used in ("push", "sdma"):
+        if backend_used in ("push", "sdma", "auto"):
             try:
-                env.enable_gather(backend_used)
+                env.enable_gather("sdma" if backend_used == "sdma" else "push")
             except Exception as ex:          # noqa: BLE001 -- reported in the line, RCCL measured instead
                 print("bench.py: %s gather setup failed (%s); using rccl" % (backend_used, ex), file=sys.stderr,
                       flush=True)
-                backend_used = "rccl"
                 fallback_note = "%s setup failed: %s" % (args.gather_backend, str(ex)[:160])
-    if gather and backend_used == "rccl":
-        # the env steps on a high-priority stream, RCCL's gather on its normal-priority one.  The
-        # gather kernel (248-256 VGPRs, 37 KB LDS per workgroup) cannot share a SIMD with a k_step
-        # wave (384 of the 512 registers), so whichever is dispatched first holds the CU: with the
-        # step first, the gather of step t fills the CUs the slowest waves of step t+1 leave idle
-        # instead of keeping step t+1's workgroups off the CUs it took
+                backend_used = "rccl"
+        # the env steps on a high-priority stream (RCCL's gather runs on its normal-priority one).
+        # RCCL's gather kernel (248-256 VGPRs, 37 KB LDS per workgroup) cannot share a SIMD with a
+        # k_step wave (384 of the 512 registers), so whichever is dispatched first holds the CU:
+        # with the step first, the gather of step t fills the CUs the slowest waves of step t+1
+        # leave idle instead of keeping step t+1's workgroups off the CUs it took
         hp = torch.cuda.Stream(device=dev, priority=-1)
         hp.wait_stream(torch.cuda.current_stream())
         torch.cuda.set_stream(hp)
     stream = torch.cuda.current_stream()
     works = [None, None]
-
-    pushg = gather and backend_used in ("push", "sdma")     # a PushGather (either engine)
+    push_gather = env._push_gather
+    state = {"mode": "push" if backend_used == "auto" else backend_used}
 
     def one_step(i):
+        mode = state["mode"]
         k = env._packed_k ^ 1        # the pack buffer this step writes
-        if gather and not pushg and works[k] is not None:
+        if mode == "rccl" and works[k] is not None:
             works[k].wait()          # the gather that last read this pack buffer (stream-ordered, no host wait)
-        env.step_raw(acts[i % len(acts)])    # (push: the step itself stores its rows into every ring;
-        if pushg and backend_used == "sdma":  #  sdma: the step waits for the copies that read buffer k)
-            env.gather_outputs(backend=backend_used, async_op=True)
-        elif gather:
+        env.step_raw(acts[i % len(acts)])    # push: the step itself stores its rows into every ring;
+        if mode == "sdma":                   # sdma: the step waited for the copies that read buffer k
+            env.gather_outputs(backend="sdma", async_op=True)
+        elif mode == "rccl":
             _, works[k] = env.gather_outputs(async_op=True)
+
+    def timed_steps(count, start):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(count):
+            one_step(start + i)
+        for w in works:
+            if w is not None:
+                w.wait()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        return D.max_over_ranks(time.perf_counter() - t0, device=dev if backend in (None, "nccl") else "cpu")
 
     # the window's bookkeeping (and the first barrier) once here: their first use loads kernels /
     # builds communicators for tens of ms, and a GPU left idle that long before the window drops
@@ -374,7 +391,22 @@ def main():
     # pause that idles the GPU before the window, or starves it while the window is queued)
     gc.collect()
     gc.disable()
-    for i in range(pre):
+    done_pre = 0
+    if backend_used == "auto":
+        # pick the faster gather on this node: 2 refill periods of each (untimed, max over ranks);
+        # the push stores ride inside the steps, so RCCL's turn runs with the push detached
+        calibration = {}
+        for _ in range(2):                   # the first pair warms both paths up
+            for m in ("rccl", "push"):
+                state["mode"] = m
+                env._push_gather = push_gather if m == "push" else None
+                calibration[m + "_ms_per_step"] = timed_steps(2 * R, done_pre) / (2 * R) * 1e3
+                done_pre += 2 * R
+        backend_used = min(("push", "rccl"), key=lambda m: calibration[m + "_ms_per_step"])
+        state["mode"] = backend_used
+        env._push_gather = push_gather if backend_used == "push" else None
+        pre = max(pre, done_pre + R)
+    for i in range(done_pre, pre):
         one_step(i)
     if args.profile_only:
         for i in range(args.steps):
@@ -394,7 +426,7 @@ def main():
     for w in works:
         if w is not None:
             w.wait()
-    if pushg and backend_used == "sdma":
+    if backend_used == "sdma":
         # every rank's pushes of the window: own copies done (sync), then the barrier after which
         # every peer's copies into this rank's ring are done too (push: the rows are stored by the
         # window's own k_step launches)
@@ -404,7 +436,7 @@ def main():
     if dist:
         dist.barrier()
     gc.enable()
-    if pushg:
+    if backend_used in ("push", "sdma"):
         # the window's last gather, checked where it landed: this rank's slot holds every rank's
         # rows of the last timed step (consumer wait, then a bit-exact compare with the gloo/RCCL
         # copy of the same rows); outside the timed region
@@ -483,7 +515,9 @@ def main():
                    "process_group": {"backend": backend, "world_size": ws} if dist else None,
                    "all_gather": dict({"bytes_per_env": 4 * D.PACK_WIDTH, "async": True, "backend": backend_used},
                                       **({"engine": env._push_gather.engine, "check": gather_check}
-                                         if pushg else {}),
+                                         if backend_used in ("push", "sdma") else {}),
+                                      **({"calibration": calibration, "chosen_by": "calibration"}
+                                         if calibration else {}),
                                       **({"fallback": fallback_note} if fallback_note else {}))
                    if gather else None,
                    "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,

@@ -262,14 +262,33 @@ class PushGather(object):
         self.spin_limit = int(spin_limit)
         W, n4 = self.world, self.n * PACK_WIDTH * 4
         self.block_bytes = n4
-        self.recv_ptr = self.ops.alloc_shared(self.depth * W * n4)
-        self.seqw_ptr = self.ops.alloc_shared(self.depth * W * 4 + 64)     # + this rank's push ticket
-        self.ticket_ptr = self.seqw_ptr + self.depth * W * 4
-        mine = (self.ops.handle(self.recv_ptr), self.ops.handle(self.seqw_ptr))
+        # every rank takes part in both exchanges even after a local failure, and all raise
+        # together: a rank that gave up alone would leave the others blocked in a collective
+        mine, err = None, None
+        try:
+            self.recv_ptr = self.ops.alloc_shared(self.depth * W * n4)
+            self.seqw_ptr = self.ops.alloc_shared(self.depth * W * 4 + 64)     # + this rank's push ticket
+            mine = (self.ops.handle(self.recv_ptr), self.ops.handle(self.seqw_ptr))
+        except Exception as ex:            # noqa: BLE001 -- re-raised below, on every rank
+            err = "rank %d: %s" % (self.rank, ex)
         allh = [None] * W
-        dist.all_gather_object(allh, mine, group=group)
-        self.peer_recv = [self.recv_ptr if p == self.rank else self.ops.open(allh[p][0]) for p in range(W)]
-        self.peer_seqw = [self.seqw_ptr if p == self.rank else self.ops.open(allh[p][1]) for p in range(W)]
+        dist.all_gather_object(allh, (mine, err), group=group)
+        errs = [e for _, e in allh if e]
+        if errs:
+            raise RuntimeError("PushGather setup failed: " + "; ".join(errs))
+        self.ticket_ptr = self.seqw_ptr + self.depth * W * 4
+        self.peer_recv, self.peer_seqw = [None] * W, [None] * W
+        try:
+            for p in range(W):
+                self.peer_recv[p] = self.recv_ptr if p == self.rank else self.ops.open(allh[p][0][0])
+                self.peer_seqw[p] = self.seqw_ptr if p == self.rank else self.ops.open(allh[p][0][1])
+        except Exception as ex:            # noqa: BLE001
+            err = "rank %d: %s" % (self.rank, ex)
+        oks = [None] * W
+        dist.all_gather_object(oks, err, group=group)
+        errs = [e for e in oks if e]
+        if errs:
+            raise RuntimeError("PushGather peer mapping failed: " + "; ".join(errs))
         self.recv = self.ops.view(self.recv_ptr, (self.depth, W, self.n, PACK_WIDTH), torch.float32)
         self.seqw = self.ops.view(self.seqw_ptr, (self.depth, W), torch.int32)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)

@@ -300,3 +300,45 @@ def test_push_gather_exchange_and_layout(engine):
     # depth 3: slot 0 last held step 6 (overrun test), slot 1 step 4, slot 2 step 5
     np.testing.assert_array_equal(seqw, np.array([[6] * world, [4] * world, [5] * world]))
     assert overrun == 2
+
+
+class _FailingOps(_ShmCopyOps):
+    def open(self, handle):
+        raise OSError("peer mapping refused (test)")
+
+
+def _fail_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ctr_reach_amd import distributed as D
+        ops = _FailingOps() if rank == 1 else _ShmCopyOps()
+        try:
+            D.PushGather(8, ops=ops)
+            q.put((rank, "no error"))
+        except RuntimeError as ex:
+            q.put((rank, str(ex)))
+        for ptr, (path, mm) in list(ops.maps.items()):
+            if path.startswith("/dev/shm/ctr_ce_test_%d_" % os.getpid()):
+                os.unlink(path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_push_gather_setup_failure_raises_on_every_rank():
+    """A rank that cannot map a peer's ring makes EVERY rank raise (bench.py then falls back to
+    RCCL on all ranks) instead of leaving the others blocked in a collective."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert "peer mapping failed" in got[r] and "rank 1" in got[r], got
