@@ -13,6 +13,7 @@ TAILN=30 run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 400 python bench.py --gpus 1 --steps 20 --warmup 5
 run bench_128 300 python bench.py --steps 128 --warmup 5 --no-cpu-baseline
+run bench_obs64 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --obs-dtype float64
 run bench_n2_gloo 300 env CTR_BENCH_BACKEND=gloo CTR_BENCH_SAME_DEVICE=1 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline
 run bench_c2 300 python bench.py --config 2 --steps 20 --warmup 5 --cpu-seconds 5
 run bench_c5 300 python bench.py --config 5 --steps 20 --warmup 5 --cpu-seconds 5

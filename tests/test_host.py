@@ -82,7 +82,8 @@ def test_struct_layout_matches_header(tmp_path):
     from ctr_reach_amd import _abi
     structs = [(_abi.CtrSystem, "ctr_system_t"), (_abi.CtrTubeRaw, "ctr_tube_raw_t"),
                (_abi.CtrEnvConfig, "ctr_env_config_t"), (_abi.CtrBatch, "ctr_batch_t"),
-               (_abi.CtrStepOut, "ctr_step_out_t"), (_abi.CtrHer, "ctr_her_t"), (_abi.CtrHerBatch, "ctr_her_batch_t")]
+               (_abi.CtrStepOut, "ctr_step_out_t"), (_abi.CtrHer, "ctr_her_t"), (_abi.CtrHerBatch, "ctr_her_batch_t"),
+               (_abi.CtrCopy, "ctr_copy_t"), (_abi.CtrGatherPush, "ctr_gather_push_t")]
     lines, want = [], []
     for cls, cname in structs:
         lines.append('  printf("%%zu\\n", sizeof(%s));' % cname)
