@@ -60,6 +60,9 @@ struct KCfg {
     int32_t mode;       // fk_dispatch MODE bits
 };
 
+// LUT = false: skip the per-description segment table (SysK::lut stays NULL; seg_par_at then
+// derives the row itself), for kernels whose FK never reads it (the rigid 8-lane group path).
+template <bool LUT = true>
 __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr)
 {
     constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
@@ -76,6 +79,11 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tub
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kc.c.n_systems * 11; i += blockDim.x) sysk_derive(lds[i / 11], i % 11);
+    if (!LUT) {
+        for (int i = threadIdx.x; i < kc.c.n_systems; i += blockDim.x) lds[i].lut = nullptr;
+        __syncthreads();
+        return;
+    }
     __syncthreads();
     // seg_par of every (system, 6-bit gap description): SysK::lut, read at segment starts
     __shared__ double s_lut[CTR_MAX_SYSTEMS][64][8];
@@ -367,11 +375,15 @@ struct PoolPre {
     double dg[3], ag[3];
 };
 
+// ALL: load every env's next reset, not only the time-limit ones (the rigid 8-lane group path:
+// latency-bound, with registers to spare, and its successes are as likely to sit on the slowest
+// wave's tail).
+template <bool ALL = false>
 __device__ __forceinline__ void pool_prefetch(const KCfg &kc, const ctr_batch_t &b, int64_t e, int32_t autoreset,
                                               PoolPre &pp)
 {
     const int P = b.pool_depth;
-    if (!autoreset || P <= 0 || b.t[e] + 1 < kc.c.max_steps) return;
+    if (!autoreset || P <= 0 || (!ALL && b.t[e] + 1 < kc.c.max_steps)) return;
     const uint32_t r = b.epoch[e] + 1;
     const int64_t ps = (int64_t)(r % (uint32_t)P) * b.n + e;
     pp.loaded = true;
@@ -491,6 +503,104 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
     if (o.status) o.status[e] = stat;
 }
 
+// step_finish for the rigid 8-lane group path (no HER): the env's two observations -- of the
+// post-step state (lane 0: the terminal one of a done env) and of the pooled reset's state (lane
+// 1) -- come from ONE obs_lane call with per-lane operands instead of two calls in sequence on the
+// lead lane; lane 1 also holds the env's prefetched pool row (pool_prefetch<true>) and writes the
+// reset, lane 0 everything else.  Same values and the same flags as step_finish.  Every lane of
+// the wave calls it (group shuffles); ag is valid on lane 0 of the group (fk_group_rigid4).
+__device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o,
+                                                  int64_t e, int j, bool in, int s, const float q[6], double ag[3],
+                                                  const FkStats &st, int32_t autoreset, StepFlags &fl,
+                                                  const PoolPre &pp)
+{
+    const int lead = (int)(threadIdx.x & 63) & ~(SEG_GROUP - 1);
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) ag[i] = __shfl(ag[i], lead);
+    if (!in || j > 1) return;
+    const int32_t t = b.t[e] + 1;
+    double dg[3];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) dg[i] = b.desired_goal[3 * e + i];
+    const double dx = ag[0] - dg[0], dy = ag[1] - dg[1], dz = ag[2] - dg[2];
+    const double d = sqrt(dx * dx + dy * dy + dz * dz);
+    const double tol = kc.c.tol;
+    const float reward = (d > tol) ? -1.0f : 0.0f;              // ctr_reach_env.py:170
+    const bool done = (reward == 0.0f) || (t >= kc.c.max_steps); // :140
+    const bool multi = kc.c.n_systems > 1;
+    const bool f64 = kc.c.obs_f64 != 0;
+    const uint32_t r = b.epoch[e] + 1;                          // reset number to take
+    // lane 1 holds the prefetched row of reset r: a pooled reset if the env is done and it is there
+    const bool reset = autoreset && done && b.pool_depth > 0 && j == 1 && pp.loaded && pp.pr == r;
+    // lanes 0 and 1 of the group agree on the reset (shuffled while both are active)
+    const bool reset_env = __shfl(reset ? 1 : 0, lead + 1) != 0;
+    const uint32_t reset_stat = (uint32_t)__shfl(reset ? (int)pp.stat : 0, lead + 1);
+    float qo[6];
+    double dgo[3], ago[3];
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) qo[i] = reset ? pp.q0[i] : q[i];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { dgo[i] = reset ? pp.dg[i] : dg[i]; ago[i] = reset ? pp.ag[i] : ag[i]; }
+    const int so = reset ? clamp_sys(pp.sys, kc.c.n_systems) : s;
+    double obs[14];
+    obs_lane(qo, dgo, ago, tol, so, multi, kc.c.egocentric != 0, obs);
+    if (j == 0) {
+        o.reward[e] = reward;
+        o.done[e] = done ? 1 : 0;
+        o.success[e] = (d < tol) ? 1 : 0;                       // :155
+        o.error[e] = (float)d;
+        if (o.nfev) o.nfev[e] = st.nfev;
+        if (o.packed || o.gather) {
+            const float fl4 = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0) | ((reward < 0.0f) ? 4 : 0));
+            const float4 row = make_float4((float)ag[0], (float)ag[1], (float)ag[2], fl4);
+            if (o.packed) *reinterpret_cast<float4 *>(o.packed + 4 * e) = row;
+            if (o.gather) gather_store_row(o.gather, e, row);
+        }
+        uint32_t stat = st.status;
+        if (autoreset && done) {
+            if (o.terminal_obs) write_obs(o.terminal_obs, e, obs, multi, f64);
+            if (o.terminal_achieved)
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
+            if (!reset_env) {
+                if (autoreset == CTR_AUTORESET_POOLED) stat |= CTR_STATUS_POOL_MISS;   // see step_finish
+                else fl.miss = true;
+            }
+        }
+        if (reset_env) stat |= reset_stat;
+        else {
+            b.t[e] = t;
+            #pragma unroll
+            for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = q[i];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) b.achieved_goal[3 * e + i] = ag[i];
+            write_obs(o.obs, e, obs, multi, f64);
+        }
+        if (o.status) o.status[e] = stat;
+    } else if (reset) {
+        // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
+        if (b.desired_joints)
+            #pragma unroll
+            for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = pp.qd[i];
+        if (b.starting_joints)
+            #pragma unroll
+            for (int i = 0; i < 6; ++i) b.starting_joints[6 * e + i] = pp.q0[i];
+        if (b.starting_position)
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) b.starting_position[3 * e + i] = pp.ag[i];
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) { b.desired_goal[3 * e + i] = pp.dg[i]; b.achieved_goal[3 * e + i] = pp.ag[i]; }
+        #pragma unroll
+        for (int i = 0; i < 6; ++i) b.joints[6 * e + i] = pp.q0[i];
+        b.system[e] = so;
+        b.epoch[e] = r;
+        b.t[e] = 0;
+        write_obs(o.obs, e, obs, multi, f64);
+        fl.pooled = true;
+        fl.pooled_r = r;
+    }
+}
+
 // Torsionally rigid model with fixed-step RK4 (MODE bits 2 and 4): one env on a group of
 // SEG_GROUP lanes, whose segments run in parallel (fk_group_rigid4); other modes: one env per lane.
 // HER: record the step into the HER store (ctr_step_her); a compile-time switch, so the plain
@@ -504,7 +614,7 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     constexpr int G = GROUP ? SEG_GROUP : 1;
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
-    stage_systems(kc, s_sys, s_raw);
+    stage_systems<!GROUP>(kc, s_sys, s_raw);
     const int64_t gl = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const int64_t e = gl / G;
     const int j = (int)(gl % G);
@@ -521,6 +631,10 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         // every lane of the wave takes part in the group's shuffles
         int s = 0;
         float q[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        PoolPre pp;
+        // the env's next reset, in flight during set_action (lane 1 writes pooled resets without
+        // HER; the lead lane with it)
+        if (in && j == (HER ? 0 : 1)) pool_prefetch<true>(kc, b, e, autoreset, pp);
         if (in) {
             s = clamp_sys(b.system[e], kc.c.n_systems);
             float a[6];
@@ -528,8 +642,6 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
             set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
         }
-        PoolPre pp;
-        if (live) pool_prefetch(kc, b, e, autoreset, pp);
         const SysK &sy = in ? episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)) : s_sys[0];
         const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
         FkStats st = {0, 0, 0, 0, 0};
@@ -538,7 +650,11 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             fk_group_rigid4<(MODE & 1) != 0, true>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
         else
             fk_group_rigid4<(MODE & 1) != 0, false>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
-        if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
+        if constexpr (HER) {
+            if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
+        } else {
+            step_finish_group(kc, b, o, e, j, in, s, q, ag, st, autoreset, fl, pp);
+        }
     } else if (live) {
         const int s = clamp_sys(b.system[e], kc.c.n_systems);
         const SysK &sy = s_sys[s];
@@ -790,17 +906,37 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     }
 }
 
-// Requeue: every env's resets epoch + 1 .. epoch + P that its pool slots do not hold.
+// Requeue: every env's resets epoch + 1 .. epoch + P that its pool slots do not hold (after a seed
+// change or a restore).  One atomic per wave: each lane counts its missing resets (a bit mask over
+// j), an exclusive prefix sum over the wave places them.
 __global__ __launch_bounds__(BLOCK) void k_pool_requeue(ctr_batch_t b)
 {
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool in = e < b.n;
     const uint32_t r = in ? b.epoch[e] : 0u;
-    for (int j = 1; j <= b.pool_depth; ++j) {
+    const int P = b.pool_depth;
+    uint64_t miss = 0;                 // bit j - 1: reset r + j missing (P <= 64)
+    for (int j = 1; j <= P && in; ++j) {
         const uint32_t rr = r + (uint32_t)j;
-        const bool need = in && b.pool_r[(int64_t)(rr % (uint32_t)b.pool_depth) * b.n + e] != rr;
-        const int32_t two[2] = {(int32_t)e, (int32_t)rr};
-        wave_append(b.refill, b.refill + 1, b.refill_cap, need, two, 2);
+        if (b.pool_r[(int64_t)(rr % (uint32_t)P) * b.n + e] != rr) miss |= 1ull << (j - 1);
+    }
+    const int cnt = __popcll(miss);
+    const int lane = threadIdx.x & 63;
+    int incl = cnt;                    // inclusive prefix sum over the wave
+    #pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+    }
+    const int total = __shfl(incl, 63);
+    if (total == 0) return;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(b.refill, total);
+    base = __shfl(base, 0) + (incl - cnt);
+    for (uint64_t m = miss; m; m &= m - 1, ++base) {
+        if (base >= b.refill_cap) break;
+        b.refill[1 + 2 * base] = (int32_t)e;
+        b.refill[2 + 2 * base] = (int32_t)(r + 1u + (uint32_t)__builtin_ctzll(m));
     }
 }
 
@@ -855,7 +991,7 @@ int check_batch(const ctr_batch_t &b, const char *who)
     if (b.n == 0) return 0;
     if (!b.joints || !b.desired_goal || !b.achieved_goal || !b.t || !b.system || !b.epoch)
         return fail(CTR_EINVAL, who);
-    if (b.pool_depth < 0) return fail(CTR_EINVAL, "pool_depth < 0");
+    if (b.pool_depth < 0 || b.pool_depth > 64) return fail(CTR_EINVAL, "pool_depth out of range (0..64)");
     if (b.pool_depth > 0 && (!b.pool_qd || !b.pool_dg || !b.pool_q0 || !b.pool_ag || !b.pool_sys || !b.pool_r ||
                              !b.pool_stat || !b.refill || b.refill_cap <= 0))
         return fail(CTR_EINVAL, "pool_depth > 0 needs every pool buffer and a refill queue");

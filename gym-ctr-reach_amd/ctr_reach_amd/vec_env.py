@@ -177,7 +177,7 @@ class CtrReachVecEnv(object):
         # depth >= the refill interval: every env then finds its next reset in the pool on every
         # step (CTR_AUTORESET_POOLED, no miss-sweep launch); 108 B per env and slot
         if pool_depth is None:
-            pool_depth = max(8, int(refill_interval)) if (self.autoreset and self.resample_joints) else 0
+            pool_depth = max(8, min(64, int(refill_interval))) if (self.autoreset and self.resample_joints) else 0
         if pool_depth and not self.resample_joints:
             raise ValueError("the reset pool needs resample_joints=True")
         self.pool_depth = int(pool_depth)

@@ -303,6 +303,7 @@ def test_refill_writes_only_resets_the_env_can_take(cuda):
     """k_refill writes a queued (env, r) only when epoch < r <= epoch + P: two queued resets for
     one ring slot (r and r + P) can then never both be written (they would race)."""
     import torch
+    from ctr_reach_amd import _abi
     env = _env(cuda, 256, seed=3, pool_depth=2, refill_interval=1000)
     env.reset()
     torch.cuda.synchronize()
@@ -318,7 +319,9 @@ def test_refill_writes_only_resets_the_env_can_take(cuda):
     q[0] = 2
     q[1], q[2] = e, ep - 1
     q[3], q[4] = e, ep + 1
-    env.refill_pool()
+    refill_only = lambda: _abi.check(env.lib.ctr_pool_refill(env.cfg, env._batch, _abi.stream_ptr()),  # noqa: E731
+                                     "ctr_pool_refill")                  # k_refill on this queue, no scan
+    refill_only()
     torch.cuda.synchronize()
     assert int(env.pool_r[slot, e].item()) == ep + 1
     for k, v in row.items():
@@ -328,7 +331,7 @@ def test_refill_writes_only_resets_the_env_can_take(cuda):
     q.zero_()
     q[0] = 1
     q[1], q[2] = e, ep - 1
-    env.refill_pool()
+    refill_only()
     torch.cuda.synchronize()
     assert int(env.pool_r[slot, e].item()) == 0
     assert int(env.refill[0].item()) == 0                      # the refill cleared its queue
