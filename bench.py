@@ -87,6 +87,10 @@ def parse():
                          "this runtime); rccl: all_gather_into_tensor over RCCL; auto: time push and rccl on 2 "
                          "refill periods each (untimed) and run the window with the faster.  push / sdma / auto fall "
                          "back to rccl if the IPC setup fails")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="replay each refill period's steps from one captured HIP graph (CtrReachVecEnv."
+                         "capture_steps) instead of launching step by step from Python; auto: on without the "
+                         "per-step gather")
     ap.add_argument("--obs-dtype", choices=("float32", "float64"), default="float32",
                     help="stored observation dtype (computed in float64 either way; float64 = the reference's)")
     ap.add_argument("--dry-run", action="store_true",
@@ -408,6 +412,15 @@ def main():
         pre = max(pre, done_pre + R)
     for i in range(done_pre, pre):
         one_step(i)
+    use_graph = args.graph == "on" or (args.graph == "auto" and not gather)
+    graph = None
+    if use_graph:
+        # one refill period (R steps, the pool refill at its end) captured once; the window replays
+        # it steps / R times.  The capture launches nothing; two untimed replays warm the graph.
+        graph = env.capture_steps([acts[i % len(acts)] for i in range(R)])
+        for _ in range(2):
+            graph.replay()
+    R_steps = R
     if args.profile_only:
         for i in range(args.steps):
             one_step(i)
@@ -421,8 +434,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(i)
+    if graph is not None:
+        for _ in range(args.steps // R_steps):
+            graph.replay()
+    else:
+        for i in range(args.steps):
+            one_step(i)
     for w in works:
         if w is not None:
             w.wait()
@@ -520,6 +537,8 @@ def main():
                                          if calibration else {}),
                                       **({"fallback": fallback_note} if fallback_note else {}))
                    if gather else None,
+                   "launch": ("one HIP graph per refill period (%d steps + the refill), replayed" % R_steps
+                              if graph is not None else "per step from Python (ctypes -> ctr_step)"),
                    "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,
                                   "autoreset": "pooled (no miss sweep)" if env.pool_depth >= env.refill_interval
                                   else "pooled + miss sweep"},

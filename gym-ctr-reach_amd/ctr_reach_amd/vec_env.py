@@ -376,6 +376,19 @@ class CtrReachVecEnv(object):
             if self._steps_since_refill >= self.refill_interval:
                 self.refill_pool(stream)
 
+    def capture_steps(self, actions, stream=None):
+        """Capture len(actions) consecutive steps (step_raw, with the pool refills that fall due)
+        into one HIP graph; ``StepGraph.replay()`` then runs them with a single launch, so a
+        launch-bound batch (configs[1]: 4 096 envs, ~10 us kernels) is not paced by the host.
+
+        The host side of a step (buffer parities, the refill schedule, the auto-reset mode) is
+        fixed in the graph, so the sequence must bring it back to where it started: start right
+        after a refill, a multiple of refill_interval steps, an even number of steps, the pool
+        full (no miss sweeps).  Not with HER or the push gather (their sequence numbers change every
+        step).  The goal tolerance and the action buffers are captured: re-capture after
+        update_goal_tolerance, and write new actions into the captured buffers."""
+        return StepGraph(self, actions, stream)
+
     def compute_reward(self, achieved_goal, desired_goal, info=None):
         """compute_reward (ctr_reach_env.py:160-170), batched over leading dims.  Device tensors
         run on the GPU (HER relabelling); numpy arrays follow the reference exactly."""
@@ -590,3 +603,41 @@ class CtrReachVecEnv(object):
 
     def close(self):
         pass
+
+
+class StepGraph(object):
+    """A captured sequence of CtrReachVecEnv steps (CtrReachVecEnv.capture_steps)."""
+
+    def __init__(self, env, actions, stream=None):
+        torch = _torch()
+        k = len(actions)
+        if env._her is not None or env._push_gather is not None:
+            raise RuntimeError("capture_steps: not with the HER feed or the push gather")
+        if env.autoreset and env.pool_depth:
+            if k % env.refill_interval or env._steps_since_refill != 0 or not env._pool_full:
+                raise RuntimeError("capture_steps: start right after a refill with a full pool and capture a "
+                                   "multiple of refill_interval (%d) steps" % env.refill_interval)
+        elif env.autoreset:
+            raise RuntimeError("capture_steps: auto-reset needs the reset pool")
+        if k % 2:
+            raise RuntimeError("capture_steps: an even number of steps (buffer parities)")
+        self.env, self.steps = env, k
+        self.actions = [a for a in actions]
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=env.device)
+        self.stream.wait_stream(torch.cuda.current_stream(env.device))
+        refills, sweeps, seq = env.refills, env.sweeps, env.packed_seq
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            for a in self.actions:
+                env.step_raw(a, self.stream)
+        self.refills_per_replay = env.refills - refills
+        # the capture launched nothing: its host bookkeeping is undone, replay() redoes it
+        env.refills, env.sweeps, env.packed_seq = refills, sweeps, seq
+        assert env._steps_since_refill == 0 or not env.pool_depth
+
+    def replay(self):
+        """Run the captured steps (stream-ordered on the current stream, like step())."""
+        self.graph.replay()
+        self.env.refills += self.refills_per_replay
+        if self.env.packed_bufs is not None:
+            self.env.packed_seq += self.steps

@@ -10,7 +10,10 @@ sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
 from ctr_reach_amd import CtrReachVecEnv  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-env = CtrReachVecEnv(n, device="cuda", seed=0, refill_interval=1000, pool_depth=32)
+kw = {}
+if len(sys.argv) > 2 and sys.argv[2] == "rigid":      # configs[1]: rigid model, RK4 at 100 steps/m
+    kw = dict(integrator="rk4", rk4_steps_per_m=100, model="rigid")
+env = CtrReachVecEnv(n, device="cuda", seed=0, refill_interval=1000, pool_depth=32, **kw)
 env.reset()
 g0 = torch.Generator(device="cpu")
 g0.manual_seed(2)
