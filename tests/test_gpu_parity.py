@@ -441,6 +441,46 @@ def test_state_dict_roundtrip_replays_exactly(cuda, her_on):
     assert env.sweeps == 0
 
 
+def test_restore_into_an_env_with_another_seed_replays_the_checkpoint(cuda):
+    """A checkpoint saved under seed 7 and restored into an env built (and stepped) with seed 0
+    replays exactly what a seed-7 env restored from it does: the ring's seed-0 resets are dropped
+    even where their reset numbers match the restored epochs."""
+    import torch
+    n = 1024
+    kw = dict(max_steps_per_episode=3, refill_interval=4)
+    src = _env(cuda, n, seed=7, **kw)
+    src.goal_tolerance.current_tol = 0.03
+    src.reset()
+    rng = np.random.default_rng(21)
+    acts = [torch.tensor((rng.uniform(-1, 1, (n, 6)) * src.action_space.high).astype(np.float32), device=cuda)
+            for _ in range(10)]
+    for a in acts[:3]:
+        src.step(a)
+    sd = src.state_dict()
+    other = _env(cuda, n, seed=0, **kw)            # same reset numbers, the other seed's draws in its ring
+    other.goal_tolerance.current_tol = 0.03
+    other.reset()
+    for a in acts[:3]:
+        other.step(a)
+    same = _env(cuda, n, seed=7, **kw)
+    same.goal_tolerance.current_tol = 0.03
+    same.reset()
+    other.load_state_dict(sd)
+    same.load_state_dict(sd)
+    assert other.seed_value == 7
+    for a in acts[3:]:
+        other.step(a)
+        same.step(a)
+        torch.cuda.synchronize()
+        for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs"):
+            assert torch.equal(getattr(other, k), getattr(same, k)), k
+    assert int((same.epoch - sd["epoch"]).sum().item()) > n     # resets taken after the restore
+    with pytest.raises(KeyError):
+        bad = dict(sd)
+        del bad["obs"]
+        same.load_state_dict(bad)
+
+
 def test_float64_observations_round_to_the_float32_ones(cuda):
     """obs_dtype="float64" stores the same observation values the float32 env rounds once:
     two envs on the same seed and actions (auto-resets included) give obs64.float() == obs32
@@ -463,6 +503,9 @@ def test_float64_observations_round_to_the_float32_ones(cuda):
             assert torch.equal(getattr(a, k), getattr(b, k)), k
     with pytest.raises(ValueError):
         b.enable_her()
+    from ctr_reach_amd import HerReplayBuffer
+    with pytest.raises(ValueError):
+        HerReplayBuffer(b)                     # built directly: the buffer checks the dtype itself
 
 
 def test_seed_change_rekeys_the_reset_pool(cuda):
