@@ -452,6 +452,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    el_local = time.perf_counter() - t0
     gc.enable()
     if backend_used in ("push", "sdma"):
         # the window's last gather, checked where it landed: this rank's slot holds every rank's
@@ -470,7 +471,7 @@ def main():
         torch.cuda.synchronize()
         gather_check = {"last_step_rows_equal": bool(torch.equal(out, torch.cat(blocks))),
                         "wait_error": int(env._push_gather.err.item())}
-    el = D.max_over_ranks(time.perf_counter() - t0, device=dev if backend in (None, "nccl") else "cpu")
+    el = D.max_over_ranks(el_local, device=dev if backend in (None, "nccl") else "cpu")
     resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
     refills = env.refills - refills0
     sweeps = env.sweeps - sweeps0

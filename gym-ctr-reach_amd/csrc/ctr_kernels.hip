@@ -859,7 +859,8 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int64_t s_count;
     if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
-    stage_systems(kc, s_sys, s_raw);
+    // (the rigid model's FK never reads the segment LUT: no staging of it)
+    stage_systems<(MODE & 4) == 0>(kc, s_sys, s_raw);
     // entries are dealt round-robin over the waves of the first (at most) 256 workgroups, one
     // wave per SIMD of the chip: a typical refill (~10 k entries) then puts ~10 resets on every
     // wave instead of 32 on a third of them, and a wave lasts as long as its slowest lane
