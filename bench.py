@@ -91,6 +91,9 @@ def parse():
                     help="replay each refill period's steps from one captured HIP graph (CtrReachVecEnv."
                          "capture_steps) instead of launching step by step from Python; auto: on without the "
                          "per-step gather")
+    ap.add_argument("--refill-budget", type=int, default=None,
+                    help="resumable refill: RK45 iterations per reset FK and refill (default: the env's, 6; "
+                         "0 = every refill runs its FKs to the end)")
     ap.add_argument("--obs-dtype", choices=("float32", "float64"), default="float32",
                     help="stored observation dtype (computed in float64 either way; float64 = the reference's)")
     ap.add_argument("--dry-run", action="store_true",
@@ -320,7 +323,8 @@ def main():
     systems = [int(s) for s in args.systems.split(",")]
     env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
                          integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"],
-                         select_systems=systems, refill_interval=R, pack_outputs=gather, obs_dtype=args.obs_dtype)
+                         select_systems=systems, refill_interval=R, pack_outputs=gather, obs_dtype=args.obs_dtype,
+                         refill_budget=args.refill_budget if cfgd["integrator"] == "rk45_scipy" else None)
     env.reset()
     max_steps = env.max_steps_per_episode
     if not args.no_stagger:
@@ -430,6 +434,7 @@ def main():
     # ---- timed region: K whole-job steps, auto-resets and pool refills at their natural rate
     epoch0 = env.epoch.to(torch.int64).sum()
     refills0, sweeps0 = env.refills, env.sweeps
+    carried0 = sum(env.carried())                 # suspended resets the window's first refill finishes
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -541,8 +546,11 @@ def main():
                    "launch": ("one HIP graph per refill period (%d steps + the refill), replayed" % R_steps
                               if graph is not None else "per step from Python (ctypes -> ctr_step)"),
                    "reset_pool": {"depth": env.pool_depth, "refill_interval": env.refill_interval,
-                                  "autoreset": "pooled (no miss sweep)" if env.pool_depth >= env.refill_interval
-                                  else "pooled + miss sweep"},
+                                  "autoreset": "pooled (no miss sweep)" if env._pooled_steps() >= env.refill_interval
+                                  else "pooled + miss sweep",
+                                  "refill_budget": env.refill_budget,
+                                  "suspended_resets_before_window": carried0,
+                                  "suspended_resets_after_window": sum(env.carried())},
                    "steady_state": {"staggered_t": not args.no_stagger, "untimed_steps_before": pre,
                                     "resets_in_window": resets, "refills_in_window": refills * ws,
                                     "refills_in_window_per_rank": refills,

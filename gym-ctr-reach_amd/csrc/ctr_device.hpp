@@ -405,6 +405,20 @@ struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
 
+// An RK45 FK suspended at the top of its attempt loop (fk_lane<..., RESUME = true>): the state y,
+// the parked u_z of tubes 1-2, the controller and the segment cursor.  The FSAL derivative f and
+// the trig of y are not stored: both are recomputed from y on resume with the same arithmetic
+// that produced them (f = K6 of the accepted step = rhs(y); a rejection leaves f at rhs(y)), so a
+// suspended-and-resumed FK is bit-identical to an uninterrupted one.  256 B.
+struct FkSuspend {
+    double yu[3], ya[3], yr[3], yR[9], uzf[3];
+    double t, tb, ha, min_step, prev_end;
+    uint32_t remaining, k, flags, pad0;   // flags: 1 need_init, 2 new_step, 4 rejected
+    FkStats st;
+    uint32_t pad1[3];
+};
+static_assert(sizeof(FkSuspend) == 256, "FkSuspend layout");
+
 #if defined(CTR_ASM_MARKERS)
 // asm-listing build: a comment + scheduling barrier at each block boundary (instruction counts)
 #define CTR_STAMP(var)                                   \
@@ -439,8 +453,11 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
 // Forward kinematics of one lane, scipy-RK45 integrator: joints (f64; the env's float32 joints
 // promoted exactly as model.py:51 does) -> tip (f64).  RIGID: torsionally rigid variant (GJ -> inf:
 // u_z stays 0, the tube angles stay at their joint values, so the trig is computed once).
-template <bool HAS_UY, bool RIGID, bool SHAPE = false, bool CAREFUL = true>
-__device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st, ShapeOut *so = nullptr)
+// RESUME (the pool refill): start from *from when it is non-null, and after `budget` loop
+// iterations (segment start + attempt) suspend into *to and return false; true = tip written.
+template <bool HAS_UY, bool RIGID, bool SHAPE = false, bool CAREFUL = true, bool RESUME = false>
+__device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStats &st, ShapeOut *so = nullptr,
+                        const FkSuspend *from = nullptr, FkSuspend *to = nullptr, int budget = 0)
 {
     using namespace rk;
     // f's alpha part is the masked u_z of y (stage_at, and K6 -> f on acceptance): it is read
@@ -478,13 +495,54 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
     double sh_a = 0.0, sh_b = 0.0, sh_step = 0.0;   // SHAPE: the segment's t_eval linspace
     bool sh_rev = false;
     int sh_j = 0;                                   // SHAPE: next t_eval point of the segment
+    int kcur = 0, iters = 0;                        // RESUME: segment cursor, iterations run
+    if constexpr (RESUME) {
+        if (from) {
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                yu[i] = from->yu[i]; ya[i] = from->ya[i]; yr[i] = from->yr[i]; uzf[i] = from->uzf[i];
+            }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) yR[i] = from->yR[i];
+            t = from->t; tb = from->tb; ha = from->ha; min_step = from->min_step; prev_end = from->prev_end;
+            remaining = from->remaining;
+            kcur = (int)from->k;
+            need_init = (from->flags & 1u) != 0;
+            new_step = (from->flags & 2u) != 0;
+            rejected = (from->flags & 4u) != 0;
+            st = from->st;
+            ty = trig_of<CAREFUL>(ya);
+            if (!need_init) {                     // mid-segment: the segment's constants and f = rhs(y)
+                p = seg_par_at<HAS_UY, RIGID>(sy, seg_bits(sg, kcur));
+                rhs_core<HAS_UY>(p, ty, yu, yR, f.uz, f.R);
+            }
+        }
+    }
 
     for (;;) {
         CTR_STAMP(ts0);
+        if constexpr (RESUME) {
+            if (iters >= budget && !(need_init && remaining == 0)) {
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    to->yu[i] = yu[i]; to->ya[i] = ya[i]; to->yr[i] = yr[i]; to->uzf[i] = uzf[i];
+                }
+                #pragma unroll
+                for (int i = 0; i < 9; ++i) to->yR[i] = yR[i];
+                to->t = t; to->tb = tb; to->ha = ha; to->min_step = min_step; to->prev_end = prev_end;
+                to->remaining = remaining;
+                to->k = (uint32_t)kcur;
+                to->flags = (need_init ? 1u : 0u) | (new_step ? 2u : 0u) | (rejected ? 4u : 0u);
+                to->st = st;
+                return false;
+            }
+            ++iters;
+        }
         if (need_init) {
             if (remaining == 0) break;
             const int k = __builtin_ctz(remaining);
             remaining &= remaining - 1u;
+            if constexpr (RESUME) kcur = k;
             p = seg_par_at<HAS_UY, RIGID>(sy, seg_bits(sg, k));
             #pragma unroll
             for (int j = 1; j < 3; ++j) {
@@ -769,6 +827,7 @@ __device__ void fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
     }
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+    return true;
 #undef CTR_FAL
 }
 

@@ -851,16 +851,76 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
     }
 }
 
-// Pool refill: entries (env, reset number) from b.refill, two lanes per entry.
+// Resumable refill (ctr_batch_t.carry): a header, then two lists of resets whose FKs a refill
+// suspended.  Refill k reads list `parity` (resuming every reset on it) and appends to the other;
+// its last workgroup empties the list it read and flips `parity`, so HIP-graph replays of the
+// refill alternate the lists without host involvement.
+struct CarryRec {
+    FkSuspend fk[2];          // the suspended goal FK (even lane) / start FK (odd lane)
+    double tip[2][3];         // the tip of an FK that has finished
+    float qd[6], q0[6];       // the reset's sampled joints
+    int32_t e;
+    uint32_t r;
+    int32_t sys;
+    uint32_t stat;            // the pair's sampling status
+    uint32_t fstat[2];        // the status of an FK that has finished
+    uint32_t done;            // bit 0: goal FK finished, bit 1: start FK finished
+    uint32_t pad;
+};
+static_assert(sizeof(CarryRec) == 640, "CarryRec layout");
+
+struct CarryHdr {
+    int32_t count[2];         // resets on each list
+    int32_t parity;           // the list the next refill reads
+    int32_t pad[13];
+};
+static_assert(sizeof(CarryHdr) == 64, "CarryHdr layout");
+
+// One FK of a refill: the scipy-RK45 FK runs at most `budget` iterations and can start from a
+// suspended state (fk_lane RESUME); fixed-step RK4 always runs to the end.
+template <int MODE>
+__device__ __forceinline__ bool fk_refill(const KCfg &kc, const SysK &sy, const float q[6], double tip[3], FkStats &st,
+                                          const FkSuspend *from, FkSuspend *to, int budget)
+{
+    if constexpr ((MODE & 2) != 0) {
+        fk_dispatch<MODE>(kc, sy, q, tip, st);
+        return true;
+    } else {
+        constexpr bool UY = (MODE & 1) != 0, RG = (MODE & 4) != 0;
+        const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
+        if (fk_needs_careful_trig(qd)) return fk_lane<UY, RG, false, true, true>(sy, qd, tip, st, nullptr, from, to, budget);
+        return fk_lane<UY, RG, false, false, true>(sy, qd, tip, st, nullptr, from, to, budget);
+    }
+}
+
+// Pool refill: the resets suspended by the previous refill (finished here), then the entries
+// (env, reset number) queued in b.refill; two lanes per reset, as reset_pair: the even lane draws
+// the desired joints and runs the goal FK, the odd lane draws the start joints and runs the start
+// FK (ctr_reach_env.py:100-112).
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
+    constexpr bool RESUMABLE = (MODE & 2) == 0;
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
-    __shared__ int64_t s_count;
-    if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
+    __shared__ int64_t s_count, s_carried;
+    __shared__ int s_par, s_budget;
+    CarryHdr *ch = static_cast<CarryHdr *>(b.carry);
+    const bool carry_on = RESUMABLE && ch != nullptr && b.carry_cap > 0;
+    if (threadIdx.x == 0) {
+        s_count = min((int64_t)b.refill[0], b.refill_cap);
+        s_par = carry_on ? (ch->parity & 1) : 0;
+        s_carried = carry_on ? min((int64_t)ch->count[s_par], b.carry_cap) : 0;
+        // a budget only while every reset of this refill would fit on the other list
+        s_budget = (carry_on && b.refill_budget > 0 && s_count + s_carried <= b.carry_cap) ? b.refill_budget : 0;
+    }
     // (the rigid model's FK never reads the segment LUT: no staging of it)
     stage_systems<(MODE & 4) == 0>(kc, s_sys, s_raw);
+    CarryRec *recs = carry_on ? reinterpret_cast<CarryRec *>(reinterpret_cast<char *>(ch) + sizeof(CarryHdr)) : nullptr;
+    const int par = s_par;
+    const int64_t c = s_carried;
+    const CarryRec *in_list = recs ? recs + par * b.carry_cap : nullptr;
+    CarryRec *out_list = recs ? recs + (par ^ 1) * b.carry_cap : nullptr;
     // entries are dealt round-robin over the waves of the first (at most) 256 workgroups, one
     // wave per SIMD of the chip: a typical refill (~10 k entries) then puts ~10 resets on every
     // wave instead of 32 on a third of them, and a wave lasts as long as its slowest lane
@@ -869,39 +929,124 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     const int64_t per_pass = waves * 32;                  // 32 lane pairs per wave
     const int64_t my_wave = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
     const int64_t my_pair = (threadIdx.x & 63) >> 1;
-    const int64_t count = blockIdx.x < G ? s_count : 0;
+    const int64_t total = s_count + c;
+    const int64_t count = blockIdx.x < G ? total : 0;
+    const int lane = threadIdx.x & 63;
+    const bool odd = threadIdx.x & 1;
     for (int64_t base = 0; base < count; base += per_pass) {
         const int64_t i = base + my_pair * waves + my_wave;
-        const bool odd = threadIdx.x & 1;
-        const bool active = i < s_count;
-        const int64_t e = active ? b.refill[1 + 2 * i] : 0;
-        const uint32_t r = active ? (uint32_t)b.refill[2 + 2 * i] : 0;
-        const int64_t ps = active ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
+        const bool carried = i < c;                       // pair-uniform, as everything below
+        const bool queued = !carried && i < total;
+        const CarryRec *rin = carried ? in_list + i : nullptr;
+        int64_t e = 0;
+        uint32_t r = 0;
+        if (carried) {
+            e = rin->e;
+            r = rin->r;
+        } else if (queued) {
+            e = b.refill[1 + 2 * (i - c)];
+            r = (uint32_t)b.refill[2 + 2 * (i - c)];
+        }
+        const int64_t ps = (carried || queued) ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
         // only the resets the env can still take from its ring, epoch + 1 .. epoch + P.  With a
         // ring shallower than the refill interval one period can queue both r + P (the env took
         // reset r from the ring) and r + 2P (the miss sweep took r + P when the ring ran dry):
         // the two map to one slot, and writing both would race (fields of two resets mixed)
-        const uint32_t ep = active ? (uint32_t)b.epoch[e] : 0u;
-        const bool fresh = active && b.pool_r[ps] != r && r - ep - 1u < (uint32_t)b.pool_depth;
-        const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
-                                               nullptr, -1);
-        if (fresh && odd) {
+        const uint32_t lead = (queued || carried) ? r - (uint32_t)b.epoch[e] - 1u : 0u;   // resets before r
+        const bool fresh = queued && b.pool_r[ps] != r && lead < (uint32_t)b.pool_depth;
+        const uint64_t genv = (uint64_t)(b.env_base + e);
+        const int s = fresh ? sample_system(kc.c.seed, r, genv, kc.c.n_systems) : (carried ? rin->sys : 0);
+        float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        uint32_t stat = 0;
+        // the wave's new resets draw together (sample_joints_wave): every lane calls it
+        if (sample_joints_wave(s_sys[s], kc.c.seed, r, odd ? 1u : 0u, genv, fresh, qv) > 1000)
+            stat |= CTR_STATUS_SAMPLER_STUCK;
+        stat |= __shfl_xor(stat, 1);                      // the pair's sampling status
+        bool had = false;                                 // this lane's FK finished in an earlier refill
+        if (carried) {
             #pragma unroll
-            for (int k = 0; k < 6; ++k) { b.pool_qd[6 * ps + k] = ro.qd[k]; b.pool_q0[6 * ps + k] = ro.q0[k]; }
+            for (int k = 0; k < 6; ++k) qv[k] = odd ? rin->q0[k] : rin->qd[k];
+            stat = rin->stat;
+            had = ((rin->done >> (odd ? 1 : 0)) & 1u) != 0;
+        }
+        double tip[3] = {0.0, 0.0, 0.0};
+        uint32_t fst = 0;                                 // this lane's FK status
+        bool fin = true;
+        FkSuspend sv;
+        if (had) {
             #pragma unroll
-            for (int k = 0; k < 3; ++k) { b.pool_dg[3 * ps + k] = ro.dg[k]; b.pool_ag[3 * ps + k] = ro.ag[k]; }
-            b.pool_sys[ps] = ro.sys;
-            b.pool_stat[ps] = ro.stat;
+            for (int k = 0; k < 3; ++k) tip[k] = rin->tip[odd][k];
+            fst = rin->fstat[odd];
+        } else if (fresh || carried) {
+            // a reset at least refill_lead resets ahead of its env runs on the budget (again, if it
+            // was suspended before); a nearer one finishes here, before the env can need it
+            const int budget = (s_budget > 0 && lead >= (uint32_t)b.refill_lead) ? s_budget : 0x7fffffff;
+            FkStats st = {0, 0, 0, 0, 0};
+            fin = fk_refill<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, r, genv), qv, tip, st,
+                                  carried ? &rin->fk[odd] : nullptr, &sv, budget);
+            fst = st.status;
+        }
+        const bool active = fresh || carried;
+        const bool ofin = __shfl_xor((int)fin, 1) != 0;
+        double otip[3];
+        float oq[6];
+        #pragma unroll
+        for (int k = 0; k < 3; ++k) otip[k] = __shfl_xor(tip[k], 1);
+        #pragma unroll
+        for (int k = 0; k < 6; ++k) oq[k] = __shfl_xor(qv[k], 1);
+        const uint32_t ofst = __shfl_xor(fst, 1);
+        if (active && fin && ofin && odd) {               // both FKs done: the pool slot
+            #pragma unroll
+            for (int k = 0; k < 6; ++k) { b.pool_qd[6 * ps + k] = oq[k]; b.pool_q0[6 * ps + k] = qv[k]; }
+            #pragma unroll
+            for (int k = 0; k < 3; ++k) { b.pool_dg[3 * ps + k] = otip[k]; b.pool_ag[3 * ps + k] = tip[k]; }
+            b.pool_sys[ps] = s;
+            b.pool_stat[ps] = stat | fst | ofst;
             b.pool_r[ps] = r;
         }
+        if constexpr (RESUMABLE) {
+            // a pair with a suspended FK goes onto the other list (one atomic per wave)
+            const bool keep = active && !(fin && ofin);
+            const uint64_t m = __ballot(keep && odd);
+            if (m) {
+                const int leader = __builtin_ctzll(m);
+                int slot = 0;
+                if (lane == leader) slot = atomicAdd(&ch->count[par ^ 1], __popcll(m));
+                slot = __shfl(slot, leader) + __popcll(m & ((1ull << (lane | 1)) - 1ull));
+                if (keep && slot < b.carry_cap) {
+                    CarryRec *ro = out_list + slot;
+                    if (fin) {
+                        #pragma unroll
+                        for (int k = 0; k < 3; ++k) ro->tip[odd][k] = tip[k];
+                        ro->fstat[odd] = fst;
+                    } else {
+                        ro->fk[odd] = sv;
+                    }
+                    if (odd) {
+                        #pragma unroll
+                        for (int k = 0; k < 6; ++k) { ro->qd[k] = oq[k]; ro->q0[k] = qv[k]; }
+                        ro->e = (int32_t)e;
+                        ro->r = r;
+                        ro->sys = s;
+                        ro->stat = stat;
+                        ro->done = (ofin ? 1u : 0u) | (fin ? 2u : 0u);
+                    }
+                }
+            }
+        }
     }
-    // the last workgroup to finish clears the queue (every workgroup read the count at its
-    // start): a ticket at refill[1 + 2 cap] instead of a clearing launch
+    // the last workgroup to finish clears the queue and the list it read, and flips the lists
+    // (every workgroup read the counts at its start): a ticket at refill[1 + 2 cap] instead of a
+    // clearing launch
     __syncthreads();
     if (threadIdx.x == 0) {
         int32_t *ticket = b.refill + 1 + 2 * b.refill_cap;
         if (atomicAdd(ticket, 1) == (int32_t)gridDim.x - 1) {
             b.refill[0] = 0;
+            if (carry_on) {
+                ch->count[par] = 0;
+                ch->parity = par ^ 1;
+            }
             *ticket = 0;
         }
     }
@@ -996,6 +1141,8 @@ int check_batch(const ctr_batch_t &b, const char *who)
     if (b.pool_depth > 0 && (!b.pool_qd || !b.pool_dg || !b.pool_q0 || !b.pool_ag || !b.pool_sys || !b.pool_r ||
                              !b.pool_stat || !b.refill || b.refill_cap <= 0))
         return fail(CTR_EINVAL, "pool_depth > 0 needs every pool buffer and a refill queue");
+    if (b.carry && (b.carry_cap <= 0 || b.carry_cap > 0x3fffffff || b.refill_budget < 0 || b.refill_lead < 0))
+        return fail(CTR_EINVAL, "carry needs carry_cap in 1..2^30 and refill_budget, refill_lead >= 0");
     return 0;
 }
 
@@ -1184,6 +1331,12 @@ int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void 
     // grid covers one entry per env (2 lanes each); larger queues are swept grid-stride
     CTR_LAUNCH(k_refill, kc.mode, dim3(grid_for(2 * b.n)), lane_lds_bytes(kc), s, kc, b);
     return hip_check("ctr_pool_refill launch");
+}
+
+int64_t ctr_refill_carry_bytes(int64_t carry_cap)
+{
+    if (carry_cap < 0) return 0;
+    return (int64_t)sizeof(CarryHdr) + 2 * carry_cap * (int64_t)sizeof(CarryRec);
 }
 
 int ctr_pool_requeue(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream)

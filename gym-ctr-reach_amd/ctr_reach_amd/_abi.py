@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 11
+CTR_ABI_VERSION = 12
 CTR_IPC_HANDLE_BYTES = 64
 CTR_GATHER_MAX_RANKS = 16
 CTR_MAX_SYSTEMS = 8
@@ -91,6 +91,10 @@ class CtrBatch(ctypes.Structure):
         ("pool_stat", _P),
         ("refill", _P),
         ("refill_cap", ctypes.c_int64),
+        ("carry", ctypes.c_void_p),
+        ("carry_cap", ctypes.c_int64),
+        ("refill_budget", ctypes.c_int32),
+        ("refill_lead", ctypes.c_int32),
     ]
 
 
@@ -156,7 +160,7 @@ EXPORTED = ("ctr_abi_version", "ctr_last_error", "ctr_fk", "ctr_set_action", "ct
             "ctr_pool_refill", "ctr_compute_reward", "ctr_domain_params", "ctr_fk_tables", "ctr_jacobian", "ctr_fk_shape",
             "ctr_her_open", "ctr_her_record", "ctr_her_sample", "ctr_step_her", "ctr_pool_requeue",
             "ctr_ipc_get_handle", "ctr_ipc_open", "ctr_ipc_close", "ctr_seqw_alloc", "ctr_seqw_free", "ctr_copy_list",
-            "ctr_gather_wait", "ctr_gather_push", "ctr_gather_publish")
+            "ctr_gather_wait", "ctr_gather_push", "ctr_gather_publish", "ctr_refill_carry_bytes")
 
 _lib = None
 
@@ -212,6 +216,9 @@ def load(path=None):
     for fn in EXPORTED[2:]:
         if hasattr(L, fn):
             getattr(L, fn).restype = ctypes.c_int
+    if hasattr(L, "ctr_refill_carry_bytes"):       # ABI 12
+        L.ctr_refill_carry_bytes.argtypes = [i64]
+        L.ctr_refill_carry_bytes.restype = i64
     # A/B timing of an older build (tools/experiments/build_rev.sh) may name its ABI version in
     # CTR_REACH_AMD_ALLOW_ABI; only entry points both versions share may then be called
     allowed = {CTR_ABI_VERSION, int(os.environ.get("CTR_REACH_AMD_ALLOW_ABI", CTR_ABI_VERSION))}

@@ -95,7 +95,7 @@ class CtrReachVecEnv(object):
 
     def __init__(self, num_envs, device="cuda", seed=0, env_base=0, autoreset=True, record_info=True,
                  pool_depth=None, refill_interval=64, integrator="rk45_scipy", rk4_steps_per_m=100,
-                 model="compliant", pack_outputs=False, obs_dtype="float32", **kwargs):
+                 model="compliant", pack_outputs=False, obs_dtype="float32", refill_budget=None, **kwargs):
         torch = _torch()
         kw = default_kwargs()
         kw.update(kwargs)
@@ -176,12 +176,29 @@ class CtrReachVecEnv(object):
         # precomputed in batches every `refill_interval` steps and consumed by a copy
         # depth >= the refill interval: every env then finds its next reset in the pool on every
         # step (CTR_AUTORESET_POOLED, no miss-sweep launch); 108 B per env and slot
+        # resumable refill (scipy RK45 only): a reset at least one refill period ahead of its env
+        # runs at most refill_budget iterations of each FK per refill; an unfinished one is
+        # suspended and resumed (bit-identically) by the next refill, so a refill lasts about as
+        # long as the budget instead of its slowest fresh sample's FK (ctr_batch_t.carry).  The
+        # resets less than a period ahead always finish: none is due before it lands
+        R = max(1, int(refill_interval))
+        resumable = integrator == "rk45_scipy"
+        if refill_budget is None:
+            refill_budget = 6 if resumable else 0
+        if refill_budget and not resumable:
+            raise ValueError("refill_budget needs the scipy RK45 integrator")
         if pool_depth is None:
-            pool_depth = max(8, min(64, int(refill_interval))) if (self.autoreset and self.resample_joints) else 0
+            # deep enough for the budget to apply over about two refills (queued resets are
+            # P - R - 1 or more ahead); 64 slots cap the ring (108 B per env and slot)
+            want = 2 * R + 24 if refill_budget else R
+            pool_depth = max(8, min(64, want)) if (self.autoreset and self.resample_joints) else 0
         if pool_depth and not self.resample_joints:
             raise ValueError("the reset pool needs resample_joints=True")
         self.pool_depth = int(pool_depth)
-        self.refill_interval = max(1, int(refill_interval))
+        self.refill_interval = R
+        # a reset queued in a period is at least P - R - 1 ahead at the refill: budgeted if P > 2R
+        self.refill_budget = int(refill_budget) if (self.pool_depth > 2 * R) else 0
+        self.refill_lead = R
         self._steps_since_refill = 0
         # True once a refill has followed a full (re)queue of every env and every refill period
         # since has taken at most pool_depth steps (pool_depth >= refill_interval)
@@ -201,6 +218,13 @@ class CtrReachVecEnv(object):
             self.pool_qd = self.pool_dg = self.pool_q0 = self.pool_ag = None
             self.pool_sys = self.pool_r = self.pool_stat = self.refill = None
             self.refill_cap = 0
+        self.carry, self.carry_cap = None, 0
+        if P and self.refill_budget:
+            # a steady-state period queues ~15 % of the envs (R = 20, 150-step episodes); a queue
+            # longer than the list (reset(), requeue) runs without the budget.  640 B per reset
+            self.carry_cap = max(256, 2 * n)
+            nb = int(self.lib.ctr_refill_carry_bytes(self.carry_cap))
+            self.carry = torch.zeros((nb + 15) // 16 * 16, dtype=torch.uint8, device=dev)
         self._batch = _abi.CtrBatch()
         self._out = _abi.CtrStepOut()
         self._her = None          # HerReplayBuffer bound by enable_her()
@@ -219,6 +243,8 @@ class CtrReachVecEnv(object):
         b.pool_qd, b.pool_dg, b.pool_q0, b.pool_ag = p(self.pool_qd), p(self.pool_dg), p(self.pool_q0), p(self.pool_ag)
         b.pool_sys, b.pool_r, b.pool_stat = p(self.pool_sys), p(self.pool_r), p(self.pool_stat)
         b.refill, b.refill_cap = p(self.refill), self.refill_cap
+        b.carry, b.carry_cap = p(self.carry), self.carry_cap
+        b.refill_budget, b.refill_lead = self.refill_budget, self.refill_lead
         o = self._out
         o.obs, o.reward, o.done, o.success, o.error = (p(self.obs), p(self.reward), p(self.done), p(self.success),
                                                         p(self.error))
@@ -256,11 +282,25 @@ class CtrReachVecEnv(object):
         """Drop the refill queue and queue every env's next pool_depth resets the pool does not
         hold (ctr_pool_requeue), then refill: after a seed change or a checkpoint restore."""
         self.refill[0] = 0
+        if self.carry is not None:
+            self.carry.zero_()           # suspended resets: the requeue below queues them again
         rc = self.lib.ctr_pool_requeue(self.cfg, self._batch, _abi.stream_ptr(stream))
         _abi.check(rc, "ctr_pool_requeue")
         self._steps_since_refill = 0
         self.refill_pool(stream)
-        self._pool_full = self.pool_depth >= self.refill_interval
+        self._pool_full = self._pooled_steps() >= self.refill_interval
+
+    def _pooled_steps(self):
+        # steps after a refill for which every env's next resets are in the pool: pool_depth, or
+        # with the resumable refill the resets less than refill_lead ahead (the ones it finishes)
+        return min(self.pool_depth, self.refill_lead) if self.carry is not None else self.pool_depth
+
+    def carried(self):
+        """Resets on the two suspended lists (resumable refill; diagnostics, synchronises)."""
+        if self.carry is None:
+            return (0, 0)
+        c = self.carry[:8].view(_torch().int32).tolist()
+        return (c[0], c[1])
 
     def refill_pool(self, stream=None):
         """Precompute the queued resets into the pool (ctr_pool_refill); asynchronous."""
@@ -268,7 +308,7 @@ class CtrReachVecEnv(object):
             rc = self.lib.ctr_pool_refill(self.cfg, self._batch, _abi.stream_ptr(stream))
             _abi.check(rc, "ctr_pool_refill")
             self.refills += 1
-            if self._steps_since_refill > self.pool_depth:
+            if self._steps_since_refill > self._pooled_steps():
                 self._pool_full = False      # a period longer than the pool: misses were swept
         self._steps_since_refill = 0
 
@@ -302,8 +342,8 @@ class CtrReachVecEnv(object):
             steps = self._steps_since_refill
             self.refill_pool(stream)
             if m is None:
-                self._pool_full = self.pool_depth >= self.refill_interval
-            elif steps > self.pool_depth:
+                self._pool_full = self._pooled_steps() >= self.refill_interval
+            elif steps > self._pooled_steps():
                 self._pool_full = False
         else:
             self._steps_since_refill = 0
@@ -352,7 +392,7 @@ class CtrReachVecEnv(object):
             # a refill that left every env's next pool_depth resets precomputed (one reset per env
             # and step): no miss-sweep launch then.  With pool_depth >= refill_interval that holds
             # on every step once reset() (or a requeue) has filled the pool.
-            if self._pool_full and self._steps_since_refill < self.pool_depth:
+            if self._pool_full and self._steps_since_refill < self._pooled_steps():
                 mode = _abi.AUTORESET_POOLED
             else:
                 mode = _abi.AUTORESET_SWEEP

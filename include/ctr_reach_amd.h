@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 11
+#define CTR_ABI_VERSION 12
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -162,6 +162,18 @@ typedef struct ctr_batch_t {
     int32_t  *refill;            /* [2 + 2 refill_cap]: count, (env, reset number) pairs,
                                     then a completion ticket (zero-initialised)          */
     int64_t   refill_cap;
+    /* Resumable refill (optional, carry NULL disables it; scipy-RK45 integrator only).  A
+     * reset at least refill_lead resets ahead of its environment (r - epoch - 1 >= refill_lead
+     * at the time of the refill) runs at most refill_budget iterations (segment start + RK45
+     * attempt) of each of its two FKs in one ctr_pool_refill; an unfinished one is suspended
+     * into the carry list and resumed by the next ctr_pool_refill, which writes its pool slot
+     * once both FKs are done.  The result is bit-identical; only the refill a reset lands in
+     * changes.  With refill_lead >= the steps between refills, no reset is due before it lands
+     * (after every refill, the resets fewer than refill_lead ahead are in the pool).  */
+    void     *carry;             /* ctr_refill_carry_bytes(carry_cap) B, zero-initialised */
+    int64_t   carry_cap;         /* resets each of its two lists holds                 */
+    int32_t   refill_budget;     /* iterations per FK and refill (0 = no budget)      */
+    int32_t   refill_lead;
 } ctr_batch_t;
 
 typedef struct ctr_gather_push_t ctr_gather_push_t;   /* defined with the push gather below */
@@ -353,6 +365,10 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
  * consumed, and by ctr_reset for the P resets after the one it computes), then clear the
  * queue.  Call it every few steps; it is a no-op when the queue is empty. */
 int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
+
+/* Bytes of batch->carry for carry_cap resets per list (a header, then two lists of suspended
+ * resets); counts[2] at byte 0 of the header give the resets each list holds (diagnostics). */
+int64_t ctr_refill_carry_bytes(int64_t carry_cap);
 
 /* Queue every environment's next pool_depth resets (epoch + 1 .. epoch + P) that its pool slots
  * do not hold, e.g. after the batch state was restored from a checkpoint or the seed changed;

@@ -337,24 +337,32 @@ def test_refill_writes_only_resets_the_env_can_take(cuda):
     assert int(env.refill[0].item()) == 0                      # the refill cleared its queue
 
 
-@pytest.mark.parametrize("depth,interval,rand", [(4, 8, 0.0), (1, 1000, 0.0), (2, 3, 0.0), (4, 8, 0.05),
-                                                  (8, 4, 0.0), (5, 5, 0.05), (1, 4, 0.0), (2, 7, 0.0)])
-def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
+@pytest.mark.parametrize("depth,interval,rand,budget", [
+    (4, 8, 0.0, None), (1, 1000, 0.0, None), (2, 3, 0.0, None), (4, 8, 0.05, None), (8, 4, 0.0, None),
+    (5, 5, 0.05, None), (1, 4, 0.0, None), (2, 7, 0.0, None),
+    # resumable refill (P > 2R): FKs suspended after `budget` iterations, finished by the next refill
+    (None, 4, 0.0, None), (None, 4, 0.05, 1), (16, 3, 0.0, 3), (None, 1, 0.0, 1)])
+def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand, budget):
     """Pooled auto-resets (precomputed ahead of time, consumed by a copy; including pool misses
     that fall back to the synchronous path) give bit-identical trajectories to computing every
     reset at the step that needs it: a reset is a pure function of (seed, env id, reset number).
     depth >= interval: every step runs CTR_AUTORESET_POOLED (no miss sweep launched at all).
     depth < interval: one refill period queues several resets for the same ring slot (taken from
     the ring, then swept after the ring ran dry); the refill writes only the ones the env can
-    still take (an intermittent mixed-slot race before that rule)."""
+    still take (an intermittent mixed-slot race before that rule).
+    depth > 2 interval (the resumable refill): resets suspended by one refill land with the next,
+    never after they are due (no sweep, no CTR_STATUS_POOL_MISS) and bit-identical."""
     import torch
     n = 4096
     kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3], domain_rand=rand)
     a = _env(cuda, n, pool_depth=0, **kw)
-    b = _env(cuda, n, pool_depth=depth, refill_interval=interval, **kw)
+    b = _env(cuda, n, pool_depth=depth, refill_interval=interval, refill_budget=budget, **kw)
+    resumable = b.carry is not None
+    assert resumable == (b.pool_depth > 2 * interval)
     a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03   # plenty of early successes
     a.reset(); b.reset()
     rng = np.random.default_rng(4)
+    carried = 0
     for _ in range(13):
         act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * a.action_space.high).astype(np.float32), device=cuda)
         oa, ra, da, ia = a.step(act)
@@ -363,9 +371,12 @@ def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand):
         for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs", "terminal_obs"):
             np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(), err_msg=k)
         assert not (b.status.cpu().numpy() & 16).any()          # CTR_STATUS_POOL_MISS never raised
+        carried = max(carried, sum(b.carried()))
     assert (a.epoch.cpu().numpy() >= 4).all()
     assert a.sweeps == 13                                         # no pool: every step sweeps
-    if depth >= interval:
+    if resumable:
+        assert carried > 0 and b.sweeps == 0                      # suspended resets, none missed
+    elif b.pool_depth >= interval:
         assert b.sweeps == 0
     else:
         assert b.sweeps > 0

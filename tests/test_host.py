@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "ctr_reach_amd.h")
 
 def _declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(ctr_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(ctr_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,7 +1,9 @@
 """Soak check of the reset pool (GPU): 150 steps of 8 192 envs with a reset roughly every other
 step, pooled auto-resets (several ring depths / refill intervals, domain randomisation) against
 synchronous resets, every state array compared bit for bit every 10 steps.  A longer cousin of
-tests/test_gpu_parity.py::test_reset_pool_matches_synchronous_resets for rare races."""
+tests/test_gpu_parity.py::test_reset_pool_matches_synchronous_resets for rare races.  The last
+configurations run the resumable refill (pool depth > 2 x interval: FKs suspended after `budget`
+iterations and resumed by later refills); no CTR_STATUS_POOL_MISS may appear."""
 import os
 import sys
 
@@ -12,26 +14,35 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from ctr_reach_amd import CtrReachVecEnv  # noqa: E402
 cuda = torch.device("cuda", 0)
 n = 8192
-configs = [(0, 1, 0.0), (2, 3, 0.0), (1, 4, 0.05), (3, 7, 0.0), (5, 5, 0.05), (8, 4, 0.0)]
+configs = [(0, 1, 0.0, 0), (2, 3, 0.0, 0), (1, 4, 0.05, 0), (3, 7, 0.0, 0), (5, 5, 0.05, 0), (8, 4, 0.0, 0),
+           (None, 4, 0.0, 6), (None, 2, 0.05, 3), (40, 5, 0.0, 2), (None, 10, 0.0, 6)]
 bad = 0
-for depth, interval, rand in configs:
-    kw = dict(seed=5 + depth, max_steps_per_episode=5, select_systems=[0, 1, 2, 3], domain_rand=rand)
+for depth, interval, rand, budget in configs:
+    kw = dict(seed=5 + (depth or 0), max_steps_per_episode=5, select_systems=[0, 1, 2, 3], domain_rand=rand,
+              refill_budget=budget)
     a = CtrReachVecEnv(n, device=cuda, pool_depth=0, **kw)
-    b = CtrReachVecEnv(n, device=cuda, pool_depth=depth, refill_interval=interval, **kw) if depth else \
+    b = CtrReachVecEnv(n, device=cuda, pool_depth=depth, refill_interval=interval, **kw) if depth != 0 else \
         CtrReachVecEnv(n, device=cuda, pool_depth=8, refill_interval=3, **kw)
+    carried = 0
     a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.04
     a.reset(); b.reset()
-    rng = np.random.default_rng(depth * 7 + interval)
+    rng = np.random.default_rng((depth or 0) * 7 + interval)
     for step in range(150):
         act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * a.action_space.high).astype(np.float32), device=cuda)
         a.step(act); b.step(act)
+        if b.carry is not None:
+            carried = max(carried, sum(b.carried()))
         if step % 10 == 9:
             torch.cuda.synchronize()
+            if (b.status & 16).any():
+                bad += 1
+                print("POOL MISS", depth, interval, rand, step, flush=True)
             for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs"):
                 if not torch.equal(getattr(a, k), getattr(b, k)):
                     bad += 1
                     print("MISMATCH", depth, interval, rand, step, k, flush=True)
                     break
-    print("config", depth, interval, rand, "resets", int(a.epoch.sum().item()), "ok" if bad == 0 else "bad", flush=True)
+    print("config", depth, interval, rand, budget, "resets", int(a.epoch.sum().item()), "max suspended", carried,
+          "ok" if bad == 0 else "bad", flush=True)
 print("TOTAL BAD", bad)
 sys.exit(1 if bad else 0)
