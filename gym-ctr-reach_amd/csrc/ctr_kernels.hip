@@ -702,8 +702,11 @@ __global__ __launch_bounds__(BLOCK) void k_step_her(KCfg kc, ctr_batch_t b, cons
 // ------------------------------------------------------------------------------------------
 // One reset (reset number r of global env genv) computed by a lane PAIR: the even lane draws the
 // desired joints and runs the goal FK (ctr_reach_env.py:100-101), the odd lane draws the start
-// joints and runs the start FK (:104-112); results are swapped with lane shuffles.  Every lane
-// of the wave must call this (inactive lanes with active = false).
+// joints and runs the start FK (:104-112); results are swapped with lane shuffles.  With the rigid
+// model and fixed-step RK4 (the 8-lane group FK of k_step, fk_group_rigid4) each FK runs on an
+// 8-lane group instead, and a reset takes 16 lanes: lanes 0-7 the goal FK, 8-15 the start FK (the
+// groups' lead lanes draw) -- so pooled and swept resets are the same arithmetic as each other.
+// Every lane of the wave must call this (inactive lanes with active = false).
 struct ResetOut {
     float qd[6], q0[6];
     double dg[3], ag[3];
@@ -712,11 +715,26 @@ struct ResetOut {
 };
 
 template <int MODE>
+struct ResetLanes {
+    static constexpr bool GROUP = (MODE & 6) == 6;
+    static constexpr int U = GROUP ? 2 * SEG_GROUP : 2;     // lanes per reset
+    static constexpr int PX = GROUP ? SEG_GROUP : 1;        // lane xor: the other FK's lane
+    // this lane's FK (0 goal, 1 start), its place in the FK's group, and whether it writes
+    __device__ static bool odd() { return ((threadIdx.x & 63) / PX) & 1; }
+    __device__ static int j() { return GROUP ? (int)(threadIdx.x & (SEG_GROUP - 1)) : 0; }
+    __device__ static bool writer() { return odd() && j() == 0; }
+};
+
+template <int MODE>
 __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys, const ctr_tube_raw_t *s_raw,
                                                bool active, bool odd,
                                                uint64_t genv, uint32_t r, const float *q_cur, const double *goal,
                                                int sys_fixed)
 {
+    using RL = ResetLanes<MODE>;
+    constexpr int PX = RL::PX;
+    const int j = RL::j();
+    const int lead = (int)(threadIdx.x & 63) - j;          // the FK group's lead lane
     const uint64_t seed = kc.c.seed;
     const int ns = kc.c.n_systems;
     const int s = !active ? 0 : (sys_fixed >= 0 ? sys_fixed : sample_system(seed, r, genv, ns));
@@ -724,14 +742,37 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
     uint32_t stat = 0;
     float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     double tip[3] = {0.0, 0.0, 0.0};
-    const bool sample = active && (odd ? (kc.c.resample_joints != 0) : (goal == nullptr));
+    const bool drew = active && (odd ? (kc.c.resample_joints != 0) : (goal == nullptr));
     // the whole wave samples together (sample_joints_wave): every lane calls it
-    if (sample_joints_wave(sy, seed, r, odd ? 1u : 0u, genv, sample, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
-    if (active) {
-        if (!sample && odd) {
+    if (sample_joints_wave(sy, seed, r, odd ? 1u : 0u, genv, drew && j == 0, qv) > 1000) stat |= CTR_STATUS_SAMPLER_STUCK;
+    if constexpr (RL::GROUP) {
+        #pragma unroll
+        for (int k = 0; k < 6; ++k) qv[k] = __shfl(qv[k], lead);
+        stat = (uint32_t)__shfl((int)stat, lead);
+    }
+    if (active && !drew && odd) {
+        #pragma unroll
+        for (int k = 0; k < 6; ++k) qv[k] = q_cur[k];
+    }
+    if constexpr (RL::GROUP) {
+        // every lane runs the group FK (DPP joins); the tip is valid on the group's lead lane
+        const SysK &esy = active ? episode_sys(kc, s_sys, s_raw, s, r, genv) : s_sys[0];
+        const double qd[6] = {(double)qv[0], (double)qv[1], (double)qv[2], (double)qv[3], (double)qv[4], (double)qv[5]};
+        FkStats st = {0, 0, 0, 0, 0};
+        if (fk_needs_careful_trig(qd))
+            fk_group_rigid4<(MODE & 1) != 0, true>(esy, qd, j, tip, st, (double)kc.c.rk4_steps_per_m);
+        else
+            fk_group_rigid4<(MODE & 1) != 0, false>(esy, qd, j, tip, st, (double)kc.c.rk4_steps_per_m);
+        #pragma unroll
+        for (int k = 0; k < 3; ++k) tip[k] = __shfl(tip[k], lead);
+        const uint32_t fst = (uint32_t)__shfl((int)st.status, lead);
+        if (active && !odd && goal) {
             #pragma unroll
-            for (int k = 0; k < 6; ++k) qv[k] = q_cur[k];
+            for (int k = 0; k < 3; ++k) tip[k] = goal[k];
+        } else if (active) {
+            stat |= fst;
         }
+    } else if (active) {
         if (!odd && goal) {
             #pragma unroll
             for (int k = 0; k < 3; ++k) tip[k] = goal[k];
@@ -744,17 +785,17 @@ __device__ __forceinline__ ResetOut reset_pair(const KCfg &kc, const SysK *s_sys
     ResetOut ro;
     #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double other = __shfl_xor(tip[k], 1);
+        const double other = __shfl_xor(tip[k], PX);
         ro.dg[k] = odd ? other : tip[k];
         ro.ag[k] = odd ? tip[k] : other;
     }
     #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const float other = __shfl_xor(qv[k], 1);
+        const float other = __shfl_xor(qv[k], PX);
         ro.qd[k] = odd ? other : qv[k];
         ro.q0[k] = odd ? qv[k] : other;
     }
-    ro.stat = stat | __shfl_xor(stat, 1);
+    ro.stat = stat | __shfl_xor(stat, PX);
     ro.sys = s;
     return ro;
 }
@@ -782,10 +823,12 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
         s_count = 0;
     }
     stage_systems(kc, s_sys, s_raw);
-    const int64_t stride = (mode == 0) ? (int64_t)gridDim.x * (BLOCK / 2) : (int64_t)1 << 62;
-    for (int64_t base = (int64_t)blockIdx.x * (BLOCK / 2); mode != 0 || base < s_count; base += stride) {
-    const int64_t slot = base + (threadIdx.x >> 1);
-    const bool odd = threadIdx.x & 1;
+    using RL = ResetLanes<MODE>;
+    constexpr int PER_WG = BLOCK / RL::U;                 // resets per workgroup and pass
+    const int64_t stride = (mode == 0) ? (int64_t)gridDim.x * PER_WG : (int64_t)1 << 62;
+    for (int64_t base = (int64_t)blockIdx.x * PER_WG; mode != 0 || base < s_count; base += stride) {
+    const int64_t slot = base + threadIdx.x / RL::U;
+    const bool odd = RL::odd();
     int64_t e = -1;
     if (mode == 0) {
         if (slot < s_count) e = miss_items(b)[slot];
@@ -802,7 +845,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
     const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, active, odd, (uint64_t)(b.env_base + ee), r, qc,
                                            goal ? goal + 3 * ee : nullptr, sf);
     bool queue = false;
-    if (active && odd) {
+    if (active && RL::writer()) {
         #pragma unroll
         for (int k = 0; k < 6; ++k) b.joints[6 * e + k] = ro.q0[k];
         #pragma unroll
@@ -924,17 +967,39 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     // entries are dealt round-robin over the waves of the first (at most) 256 workgroups, one
     // wave per SIMD of the chip: a typical refill (~10 k entries) then puts ~10 resets on every
     // wave instead of 32 on a third of them, and a wave lasts as long as its slowest lane
+    using RL = ResetLanes<MODE>;
     const int64_t G = min((int64_t)gridDim.x, (int64_t)256);
     const int64_t waves = G * (BLOCK / 64);
-    const int64_t per_pass = waves * 32;                  // 32 lane pairs per wave
+    const int64_t per_pass = waves * (64 / RL::U);        // 32 lane pairs (4 lane groups) per wave
     const int64_t my_wave = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-    const int64_t my_pair = (threadIdx.x & 63) >> 1;
+    const int64_t my_pair = (threadIdx.x & 63) / RL::U;
     const int64_t total = s_count + c;
     const int64_t count = blockIdx.x < G ? total : 0;
     const int lane = threadIdx.x & 63;
-    const bool odd = threadIdx.x & 1;
+    const bool odd = RL::odd();
     for (int64_t base = 0; base < count; base += per_pass) {
         const int64_t i = base + my_pair * waves + my_wave;
+        if constexpr (!RESUMABLE) {
+            // fixed-step RK4: every FK runs to its end (reset_pair; 8-lane group FKs for the rigid model)
+            const bool queued = i < total;
+            const int64_t e = queued ? b.refill[1 + 2 * i] : 0;
+            const uint32_t r = queued ? (uint32_t)b.refill[2 + 2 * i] : 0u;
+            const int64_t ps = queued ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
+            // only the resets the env can still take from its ring (see below)
+            const bool fresh = queued && b.pool_r[ps] != r && r - (uint32_t)b.epoch[e] - 1u < (uint32_t)b.pool_depth;
+            const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
+                                                   nullptr, -1);
+            if (fresh && RL::writer()) {
+                #pragma unroll
+                for (int k = 0; k < 6; ++k) { b.pool_qd[6 * ps + k] = ro.qd[k]; b.pool_q0[6 * ps + k] = ro.q0[k]; }
+                #pragma unroll
+                for (int k = 0; k < 3; ++k) { b.pool_dg[3 * ps + k] = ro.dg[k]; b.pool_ag[3 * ps + k] = ro.ag[k]; }
+                b.pool_sys[ps] = ro.sys;
+                b.pool_stat[ps] = ro.stat;
+                b.pool_r[ps] = r;
+            }
+            continue;
+        }
         const bool carried = i < c;                       // pair-uniform, as everything below
         const bool queued = !carried && i < total;
         const CarryRec *rin = carried ? in_list + i : nullptr;
@@ -1160,6 +1225,9 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
+// lanes k_reset / k_refill spend on one reset (ResetLanes<MODE>::U)
+inline int64_t reset_lanes(const KCfg &kc) { return (kc.mode & 6) == 6 ? 2 * SEG_GROUP : 2; }
+
 // Launch kernel template K<MODE> for the runtime mode (8 instantiations).
 #define CTR_LAUNCH(K, MODE, GRID, SHM, STREAM, ...)                                                     \
     do {                                                                                           \
@@ -1285,7 +1353,8 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset == CTR_AUTORESET_SWEEP) {
         // misses are rare with a pool: a small grid sweeps the list grid-stride
-        const unsigned g = b.pool_depth > 0 ? std::min(grid_for(2 * b.n), 64u) : grid_for(2 * b.n);
+        const unsigned g = b.pool_depth > 0 ? std::min(grid_for(reset_lanes(kc) * b.n), 64u)
+                                            : grid_for(reset_lanes(kc) * b.n);
         CTR_LAUNCH(k_reset, kc.mode, dim3(g), lane_lds_bytes(kc), s, kc, b, 0, (const uint8_t *)nullptr, (const double *)nullptr,
                    (const int32_t *)nullptr, o.obs, o.status, hk, her_on);
         return hip_check("ctr_step reset launch");
@@ -1313,7 +1382,8 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
     if (b.n == 0) return 0;
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
-    CTR_LAUNCH(k_reset, kc.mode, dim3(grid_for(2 * b.n)), lane_lds_bytes(kc), (hipStream_t)stream, kc, b, 1, mask, goal, system, obs,
+    CTR_LAUNCH(k_reset, kc.mode, dim3(grid_for(reset_lanes(kc) * b.n)), lane_lds_bytes(kc), (hipStream_t)stream, kc, b, 1, mask,
+               goal, system, obs,
                status, HerK{}, 0);
     return hip_check("ctr_reset launch");
 }
@@ -1328,8 +1398,8 @@ int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void 
     if (!cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    // grid covers one entry per env (2 lanes each); larger queues are swept grid-stride
-    CTR_LAUNCH(k_refill, kc.mode, dim3(grid_for(2 * b.n)), lane_lds_bytes(kc), s, kc, b);
+    // at most 256 workgroups (one wave per SIMD): the queued entries are dealt over their waves
+    CTR_LAUNCH(k_refill, kc.mode, dim3(std::min(grid_for(reset_lanes(kc) * b.n), 256u)), lane_lds_bytes(kc), s, kc, b);
     return hip_check("ctr_pool_refill launch");
 }
 
