@@ -178,6 +178,24 @@ def D_max_over_ranks(v):
     return D.max_over_ranks(v, device="cpu")
 
 
+def measured_traffic(n, cfgd, systems):
+    """HBM bytes per k_step launch from the PMC passes committed under profiles/ (rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE, corrected by the factors measured on k_step's own access shapes:
+    scripts/profile.sh + tools/summarize_profile.py), when they were taken on this workload; the
+    bench cannot read hardware counters itself.  (None, reason) otherwise."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, "no profiles/traffic.json"
+    if t.get("envs") != n or cfgd["integrator"] != "rk45_scipy" or cfgd["model"] != "compliant" or systems != [0]:
+        return None, "profiles/traffic.json was measured on another workload"
+    return t["bytes_per_launch"], ("profiles/traffic.json: k_step's average under rocprofv3 --pmc passes of "
+                                   "this workload, FETCH_SIZE x %.3f + WRITE_SIZE x %.3f (factors calibrated on "
+                                   "k_step's own access shapes)" % (t["read_factor"], t["write_factor"]))
+
+
 def refill_interval_for(steps, cap=64):
     """Largest divisor of the timed steps that is <= cap: the window then holds whole refill
     periods (every reset it consumes is precomputed inside it)."""
@@ -477,6 +495,7 @@ def main():
         gather_check = {"last_step_rows_equal": bool(torch.equal(out, torch.cat(blocks))),
                         "wait_error": int(env._push_gather.err.item())}
     el = D.max_over_ranks(el_local, device=dev if backend in (None, "nccl") else "cpu")
+    traffic, traffic_note = measured_traffic(n, cfgd, systems)
     resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
     refills = env.refills - refills0
     sweeps = env.sweeps - sweeps0
@@ -557,7 +576,8 @@ def main():
                                     "miss_sweep_launches_in_window_per_rank": sweeps,
                                     "mean_episode_steps_est": (total_steps / resets) if resets else None}},
         "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": PEAK_FP64_VALU, "unit": "TFLOP/s",
-                     "frac": achieved_tf / PEAK_FP64_VALU, "traffic": None,
+                     "frac": achieved_tf / PEAK_FP64_VALU, "traffic": traffic,
+                     "traffic_source": traffic_note,
                      "kernel": "k_step", "kernel_ms": k_ms,
                      "flops_per_launch": flops_env_step, "sincos_per_launch": sincos,
                      "nfev_per_env_step": nfev_mean,
