@@ -231,6 +231,25 @@ __device__ __forceinline__ void trig_table_fill()
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&s_trig_tab[0][0])[i] = (&ctr_math::TRIG_TAB[0][0])[i];
 }
 
+// The same copy in two halves, for a 256-lane workgroup: this lane's four table entries loaded
+// into registers (trig_table_load), stored to LDS later (trig_table_store), so that loads the
+// kernel issues in between overlap the table's latency instead of queueing behind its stores.
+struct TrigRegs {
+    double v[4];
+};
+
+__device__ __forceinline__ void trig_table_load(TrigRegs &t)
+{
+    #pragma unroll
+    for (int k = 0; k < 4; ++k) t.v[k] = (&ctr_math::TRIG_TAB[0][0])[threadIdx.x + k * CTR_BLOCK];
+}
+
+__device__ __forceinline__ void trig_table_store(const TrigRegs &t)
+{
+    #pragma unroll
+    for (int k = 0; k < 4; ++k) (&s_trig_tab[0][0])[threadIdx.x + k * CTR_BLOCK] = t.v[k];
+}
+
 // CAREFUL: a wave-uniform ballot sends huge / non-finite angle differences (|d| >= 2^20) to the
 // exact out-of-line path.  The branch splits the stage code into basic blocks the scheduler
 // cannot interleave (measured +6 % on k_step), so the FK checks its joint angles once

@@ -62,20 +62,54 @@ struct KCfg {
 
 // LUT = false: skip the per-description segment table (SysK::lut stays NULL; seg_par_at then
 // derives the row itself), for kernels whose FK never reads it (the rigid 8-lane group path).
-template <bool LUT = true>
-__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr)
+// The workgroup's table inputs in registers: this lane's four trig-table entries, its element of
+// the system rows and of the raw tube rows (<= 8 x 18 and 8 x 12 doubles, one per lane of a
+// 256-lane workgroup).  stage_load issues the loads; a kernel may issue its own loads before
+// stage_systems stores them, so both latencies overlap.
+struct StageRegs {
+    TrigRegs trig;
+    double sys, raw;
+};
+
+__device__ __forceinline__ void stage_load(const KCfg &kc, StageRegs &r)
 {
     constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
+    constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
+    static_assert(CTR_MAX_SYSTEMS * ND <= BLOCK && CTR_MAX_SYSTEMS * NR <= BLOCK, "one element per lane");
+    trig_table_load(r.trig);
+    const int i = (int)threadIdx.x;
+    r.sys = reinterpret_cast<const double *>(kc.c.systems)[i < kc.c.n_systems * ND ? i : 0];
+    r.raw = reinterpret_cast<const double *>(kc.c.raw)[i < kc.c.n_systems * NR ? i : 0];
+}
+
+// pre: the inputs already loaded (stage_load).
+template <bool LUT = true>
+__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr,
+                                              const StageRegs *pre = nullptr)
+{
+    constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
+    constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
     const double *src = reinterpret_cast<const double *>(kc.c.systems);
     const int nd = kc.c.n_systems * ND;
-    for (int i = threadIdx.x; i < nd; i += blockDim.x)
-        reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND]))[i % ND] = src[i];
-    trig_table_fill();
-    if (raw_lds) {
-        constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
-        const double *rs = reinterpret_cast<const double *>(kc.c.raw);
-        for (int i = threadIdx.x; i < kc.c.n_systems * NR; i += blockDim.x)
-            reinterpret_cast<double *>(raw_lds)[i] = rs[i];
+    if (pre) {
+        // unconditional stores (lanes past the rows write a dummy slot): a conditional store would
+        // let the compiler sink its load behind the caller's loads
+        __shared__ double s_stage_dummy[BLOCK];
+        const int i = (int)threadIdx.x;
+        double *ds = i < nd ? reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND])) + i % ND
+                            : &s_stage_dummy[i];
+        *ds = pre->sys;
+        trig_table_store(pre->trig);
+        if (raw_lds) *(i < kc.c.n_systems * NR ? reinterpret_cast<double *>(raw_lds) + i : &s_stage_dummy[i]) = pre->raw;
+    } else {
+        for (int i = threadIdx.x; i < nd; i += blockDim.x)
+            reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND]))[i % ND] = src[i];
+        trig_table_fill();
+        if (raw_lds) {
+            const double *rs = reinterpret_cast<const double *>(kc.c.raw);
+            for (int i = threadIdx.x; i < kc.c.n_systems * NR; i += blockDim.x)
+                reinterpret_cast<double *>(raw_lds)[i] = rs[i];
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kc.c.n_systems * 11; i += blockDim.x) sysk_derive(lds[i / 11], i % 11);
@@ -378,13 +412,14 @@ struct PoolPre {
 // ALL: load every env's next reset, not only the time-limit ones (the rigid 8-lane group path:
 // latency-bound, with registers to spare, and its successes are as likely to sit on the slowest
 // wave's tail).
+// t, epoch: the env's episode clock and reset count (already loaded by the caller).
 template <bool ALL = false>
 __device__ __forceinline__ void pool_prefetch(const KCfg &kc, const ctr_batch_t &b, int64_t e, int32_t autoreset,
-                                              PoolPre &pp)
+                                              PoolPre &pp, int32_t t, uint32_t epoch)
 {
     const int P = b.pool_depth;
-    if (!autoreset || P <= 0 || (!ALL && b.t[e] + 1 < kc.c.max_steps)) return;
-    const uint32_t r = b.epoch[e] + 1;
+    if (!autoreset || P <= 0 || (!ALL && t + 1 < kc.c.max_steps)) return;
+    const uint32_t r = epoch + 1;
     const int64_t ps = (int64_t)(r % (uint32_t)P) * b.n + e;
     pp.loaded = true;
     pp.pr = b.pool_r[ps];
@@ -405,15 +440,17 @@ struct StepFlags {
     uint32_t pooled_r = 0;
 };
 
+// t_prev, epoch, dg_prev: the env's clock, reset count and desired goal before the step (loaded
+// at the start of the step).
 __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o, int64_t e,
                                             int s, float q[6], double ag[3], const FkStats &st, int32_t autoreset,
                                             StepFlags &fl, const ctr_her_t *her, const float *action,
-                                            const PoolPre &pp)
+                                            const PoolPre &pp, int32_t t_prev, uint32_t epoch, const double dg_prev[3])
 {
-    const int32_t t = b.t[e] + 1;
+    const int32_t t = t_prev + 1;
     double dg[3];
     #pragma unroll
-    for (int i = 0; i < 3; ++i) dg[i] = b.desired_goal[3 * e + i];
+    for (int i = 0; i < 3; ++i) dg[i] = dg_prev[i];
     const double dx = ag[0] - dg[0], dy = ag[1] - dg[1], dz = ag[2] - dg[2];
     const double d = sqrt(dx * dx + dy * dy + dz * dz);
     const double tol = kc.c.tol;
@@ -450,7 +487,7 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
         if (o.terminal_achieved)
             #pragma unroll
             for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
-        const uint32_t r = b.epoch[e] + 1;                      // reset number to take
+        const uint32_t r = epoch + 1;                           // reset number to take
         const int P = b.pool_depth;
         const int64_t ps = P > 0 ? (int64_t)(r % (uint32_t)P) * b.n + e : 0;
         if (P > 0 && (pp.loaded ? pp.pr : b.pool_r[ps]) == r) {
@@ -614,12 +651,39 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     constexpr int G = GROUP ? SEG_GROUP : 1;
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
-    stage_systems<!GROUP>(kc, s_sys, s_raw);
     const int64_t gl = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const int64_t e = gl / G;
     const int j = (int)(gl % G);
     const bool in = e < b.n;                 // the lane works on a live env
     const bool live = in && j == 0;          // ... and is its lead lane (every per-env write)
+    // the table inputs' loads first, then the env's rows (system, joints, action; unconditional,
+    // from a clamped row, so nothing waits for them before the staging): the rows' latency then
+    // hides behind the tables', which the staging waits for anyway
+    StageRegs stg;
+    stage_load(kc, stg);
+    __builtin_amdgcn_sched_barrier(0);       // keep the table loads ahead of the row loads
+    const int64_t ec = in ? e : b.n - 1;
+    const int s_in = b.system[ec];
+    float q_in[6], a_in[6];
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) { q_in[i] = b.joints[6 * ec + i]; a_in[i] = actions[6 * ec + i]; }
+    const int32_t t_in = b.t[ec];
+    const uint32_t ep_in = b.epoch[ec];
+    double dg_in[3];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) dg_in[i] = b.desired_goal[3 * ec + i];
+    stage_systems<!GROUP>(kc, s_sys, s_raw, &stg);
+    // one env per lane: the finish's inputs wait out the FK in LDS (they have landed during the
+    // staging), not in registers the FK loop would have to keep
+    __shared__ double s_fin_dg[3][BLOCK];
+    __shared__ int32_t s_fin_t[BLOCK];
+    __shared__ uint32_t s_fin_ep[BLOCK];
+    if constexpr (!GROUP) {
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) s_fin_dg[i][threadIdx.x] = dg_in[i];
+        s_fin_t[threadIdx.x] = t_in;
+        s_fin_ep[threadIdx.x] = ep_in;
+    }
     // the step's sequence word after the packed rows (the copy-engine gather pushes it after them)
     if (o.packed && o.packed_seq && blockIdx.x == 0 && threadIdx.x == 0)
         *reinterpret_cast<uint4 *>(o.packed + 4 * b.n) = make_uint4(o.packed_seq, 0u, 0u, 0u);
@@ -634,13 +698,12 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         PoolPre pp;
         // the env's next reset, in flight during set_action (lane 1 writes pooled resets without
         // HER; the lead lane with it)
-        if (in && j == (HER ? 0 : 1)) pool_prefetch<true>(kc, b, e, autoreset, pp);
+        if (in && j == (HER ? 0 : 1)) pool_prefetch<true>(kc, b, e, autoreset, pp, t_in, ep_in);
         if (in) {
-            s = clamp_sys(b.system[e], kc.c.n_systems);
-            float a[6];
+            s = clamp_sys(s_in, kc.c.n_systems);
             #pragma unroll
-            for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
-            set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
+            for (int i = 0; i < 6; ++i) q[i] = q_in[i];
+            set_action_substeps(s_sys[s], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);
         }
         const SysK &sy = in ? episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)) : s_sys[0];
         const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
@@ -651,23 +714,27 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         else
             fk_group_rigid4<(MODE & 1) != 0, false>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
         if constexpr (HER) {
-            if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
+            if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, t_in, ep_in, dg_in);
         } else {
             step_finish_group(kc, b, o, e, j, in, s, q, ag, st, autoreset, fl, pp);
         }
     } else if (live) {
-        const int s = clamp_sys(b.system[e], kc.c.n_systems);
+        const int s = clamp_sys(s_in, kc.c.n_systems);
         const SysK &sy = s_sys[s];
-        float q[6], a[6];
+        float q[6];
         #pragma unroll
-        for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * e + i]; a[i] = actions[6 * e + i]; }
+        for (int i = 0; i < 6; ++i) q[i] = q_in[i];
         PoolPre pp;
-        pool_prefetch(kc, b, e, autoreset, pp);
-        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);
+        pool_prefetch(kc, b, e, autoreset, pp, t_in, ep_in);
+        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);
         FkStats st = {0, 0, 0, 0, 0};
         double ag[3];
-        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);
-        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);
+        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e)), q, ag, st);
+        double dg_f[3];
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) dg_f[i] = s_fin_dg[i][threadIdx.x];
+        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, s_fin_t[threadIdx.x],
+                    s_fin_ep[threadIdx.x], dg_f);
     }
     if (autoreset) {
         if (autoreset == CTR_AUTORESET_POOLED) {
@@ -897,7 +964,10 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
 // Resumable refill (ctr_batch_t.carry): a header, then two lists of resets whose FKs a refill
 // suspended.  Refill k reads list `parity` (resuming every reset on it) and appends to the other;
 // its last workgroup empties the list it read and flips `parity`, so HIP-graph replays of the
-// refill alternate the lists without host involvement.
+// refill alternate the lists without host involvement.  Each list is CARRY_SUBS sub-lists with
+// their own counters (workgroup b appends to sub-list b mod CARRY_SUBS): the waves of a refill
+// all suspend at about the same time, and one counter for all 1 024 of them serialised their
+// atomics (~7 us of the refill's tail, clock-stamped build).
 struct CarryRec {
     FkSuspend fk[2];          // the suspended goal FK (even lane) / start FK (odd lane)
     double tip[2][3];         // the tip of an FK that has finished
@@ -912,12 +982,14 @@ struct CarryRec {
 };
 static_assert(sizeof(CarryRec) == 640, "CarryRec layout");
 
+constexpr int CARRY_SUBS = 32;
+
 struct CarryHdr {
-    int32_t count[2];         // resets on each list
-    int32_t parity;           // the list the next refill reads
-    int32_t pad[13];
+    int32_t count[2][CARRY_SUBS];   // resets on each sub-list of each list
+    int32_t parity;                 // the list the next refill reads
+    int32_t pad[63];
 };
-static_assert(sizeof(CarryHdr) == 64, "CarryHdr layout");
+static_assert(sizeof(CarryHdr) == 512, "CarryHdr layout");
 
 // One FK of a refill: the scipy-RK45 FK runs at most `budget` iterations and can start from a
 // suspended state (fk_lane RESUME); fixed-step RK4 always runs to the end.
@@ -948,17 +1020,47 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int64_t s_count, s_carried;
     __shared__ int s_par, s_budget;
+    __shared__ int32_t s_pref[CARRY_SUBS + 1];           // sub-list starts of the list read
     CarryHdr *ch = static_cast<CarryHdr *>(b.carry);
-    const bool carry_on = RESUMABLE && ch != nullptr && b.carry_cap > 0;
-    if (threadIdx.x == 0) {
-        s_count = min((int64_t)b.refill[0], b.refill_cap);
-        s_par = carry_on ? (ch->parity & 1) : 0;
-        s_carried = carry_on ? min((int64_t)ch->count[s_par], b.carry_cap) : 0;
-        // a budget only while every reset of this refill would fit on the other list
-        s_budget = (carry_on && b.refill_budget > 0 && s_count + s_carried <= b.carry_cap) ? b.refill_budget : 0;
+    const bool carry_on = RESUMABLE && ch != nullptr && b.carry_cap >= CARRY_SUBS;
+    const int64_t sub_cap = b.carry_cap / CARRY_SUBS;
+    // the list's parity and sub-list counts: loaded by wave 0 now, used after the staging below
+    // (its barriers do not wait for them)
+    // (both lists' counts: no load waits for the parity)
+    static_assert(2 * CARRY_SUBS == 64, "one count per lane of wave 0");
+    int par_l = 0;
+    int32_t cnt_l = 0;
+    if (threadIdx.x < 64 && carry_on) {
+        par_l = ch->parity & 1;
+        cnt_l = ch->count[threadIdx.x / CARRY_SUBS][threadIdx.x % CARRY_SUBS];
     }
+    if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
     // (the rigid model's FK never reads the segment LUT: no staging of it)
     stage_systems<(MODE & 4) == 0>(kc, s_sys, s_raw);
+    if (threadIdx.x < 64) {                               // wave 0: prefix sums of the counts read
+        int32_t incl = (int32_t)min((int64_t)__shfl(cnt_l, par_l * CARRY_SUBS + (int)(threadIdx.x % CARRY_SUBS)), sub_cap);
+        if (threadIdx.x >= CARRY_SUBS) incl = 0;
+        #pragma unroll
+        for (int off = 1; off < CARRY_SUBS; off <<= 1) {
+            const int32_t v = __shfl_up(incl, off);
+            if ((int)threadIdx.x >= off) incl += v;
+        }
+        if (threadIdx.x < CARRY_SUBS) s_pref[threadIdx.x + 1] = incl;
+        if (threadIdx.x == 0) {
+            s_pref[0] = 0;
+            s_par = par_l;
+        }
+        if (threadIdx.x == CARRY_SUBS - 1) {
+            s_carried = incl;
+            // a budget only while every sub-list can take all the pairs its workgroups may suspend
+            const int64_t G = min((int64_t)gridDim.x, (int64_t)256);
+            const int64_t per_pass = G * (BLOCK / 64) * 32;
+            const int64_t passes = (s_count + incl + per_pass - 1) / per_pass;
+            const int64_t inflow = (G + CARRY_SUBS - 1) / CARRY_SUBS * (BLOCK / 64) * 32 * passes;
+            s_budget = (carry_on && b.refill_budget > 0 && inflow <= sub_cap) ? b.refill_budget : 0;
+        }
+    }
+    __syncthreads();
     CarryRec *recs = carry_on ? reinterpret_cast<CarryRec *>(reinterpret_cast<char *>(ch) + sizeof(CarryHdr)) : nullptr;
     const int par = s_par;
     const int64_t c = s_carried;
@@ -1002,7 +1104,14 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         }
         const bool carried = i < c;                       // pair-uniform, as everything below
         const bool queued = !carried && i < total;
-        const CarryRec *rin = carried ? in_list + i : nullptr;
+        const CarryRec *rin = nullptr;
+        if (carried) {                                    // sub-list k: s_pref[k] <= i < s_pref[k + 1]
+            int lo = 0;
+            #pragma unroll
+            for (int step = CARRY_SUBS / 2; step >= 1; step >>= 1)
+                if (s_pref[lo + step] <= (int32_t)i) lo += step;
+            rin = in_list + lo * sub_cap + (i - s_pref[lo]);
+        }
         int64_t e = 0;
         uint32_t r = 0;
         if (carried) {
@@ -1076,10 +1185,11 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             if (m) {
                 const int leader = __builtin_ctzll(m);
                 int slot = 0;
-                if (lane == leader) slot = atomicAdd(&ch->count[par ^ 1], __popcll(m));
+                const int sub = blockIdx.x % CARRY_SUBS;
+                if (lane == leader) slot = atomicAdd(&ch->count[par ^ 1][sub], __popcll(m));
                 slot = __shfl(slot, leader) + __popcll(m & ((1ull << (lane | 1)) - 1ull));
-                if (keep && slot < b.carry_cap) {
-                    CarryRec *ro = out_list + slot;
+                if (keep && slot < sub_cap) {
+                    CarryRec *ro = out_list + sub * sub_cap + slot;
                     if (fin) {
                         #pragma unroll
                         for (int k = 0; k < 3; ++k) ro->tip[odd][k] = tip[k];
@@ -1109,7 +1219,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         if (atomicAdd(ticket, 1) == (int32_t)gridDim.x - 1) {
             b.refill[0] = 0;
             if (carry_on) {
-                ch->count[par] = 0;
+                for (int k = 0; k < CARRY_SUBS; ++k) ch->count[par][k] = 0;
                 ch->parity = par ^ 1;
             }
             *ticket = 0;

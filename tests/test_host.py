@@ -29,6 +29,16 @@ def test_library_exports_every_declared_symbol():
         assert re.search(r"\bT %s\b" % n, out), n
 
 
+def test_refill_carry_bytes():
+    """ctr_refill_carry_bytes (host arithmetic, no GPU): a 512-B header (counts[2][32], parity),
+    then two lists of 640-B suspended-reset records; negative capacities give 0."""
+    from ctr_reach_amd import _abi
+    lib = _abi.load()
+    for cap in (0, 1, 256, 131072):
+        assert lib.ctr_refill_carry_bytes(cap) == 512 + 2 * cap * 640
+    assert lib.ctr_refill_carry_bytes(-5) == 0
+
+
 def test_abi_rejects_bad_arguments_without_gpu():
     from ctr_reach_amd import _abi, systems
     lib = _abi.load()
