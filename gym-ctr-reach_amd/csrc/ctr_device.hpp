@@ -1321,12 +1321,14 @@ __device__ __forceinline__ void obs_lane(const float q[6], const double dg[3], c
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1)
 {
+    // each 32 x 32 -> 64-bit product as one v_mad_u64_u32 (the lo and hi halves from one
+    // instruction instead of a v_mul_lo_u32 / v_mul_hi_u32 pair: 20 % faster per Philox block on
+    // gfx950, tools/ubench/philox_mul.hip; the same bits)
     #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
-        const uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
-        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
 }
@@ -1362,6 +1364,27 @@ __device__ __forceinline__ int nth_set_bit(uint64_t m, int n)
     return pos;
 }
 
+// Per-round constants of the wave sampler for k = 1..64 unresolved lanes (k is wave-uniform, so
+// each is one scalar load): div16[k] = ceil(2^16 / k), which gives x / k = (x div16[k]) >> 16
+// exactly for 0 <= x <= 128 (checked for every k and x), and stride[k] = the bits 0, k, 2k, ...
+// below 64 (a lane's helpers are its rank + that, as a mask).
+struct SampleTabs {
+    uint32_t div16[65];
+    uint64_t stride[65];
+};
+constexpr SampleTabs make_sample_tabs()
+{
+    SampleTabs t{};
+    for (int k = 1; k <= 64; ++k) {
+        t.div16[k] = (65536u + (uint32_t)k - 1u) / (uint32_t)k;
+        uint64_t m = 0;
+        for (int i = 0; i < 64; i += k) m |= 1ull << i;
+        t.stride[k] = m;
+    }
+    return t;
+}
+__constant__ SampleTabs c_sample_tabs = make_sample_tabs();
+
 __device__ __forceinline__ int sample_joints_wave(const ctr_system_t &sy, uint64_t seed, uint32_t epoch,
                                                   uint32_t stream, uint64_t env, bool need, float q[6])
 {
@@ -1376,8 +1399,10 @@ __device__ __forceinline__ int sample_joints_wave(const ctr_system_t &sy, uint64
         const uint64_t m = __ballot(unresolved);
         if (!m) break;
         const int cnt = __popcll(m);
-        const int target = nth_set_bit(m, lane % cnt);
-        const uint32_t c = (uint32_t)__shfl((int)next, target) + (uint32_t)(lane / cnt);
+        const uint32_t dv = c_sample_tabs.div16[cnt];
+        const int lq = (int)(((uint32_t)lane * dv) >> 16);          // lane / cnt
+        const int target = nth_set_bit(m, lane - lq * cnt);          // lane % cnt
+        const uint32_t c = (uint32_t)__shfl((int)next, target) + (uint32_t)lq;
         const uint32_t t_ep = (uint32_t)__shfl((int)epoch, target);
         const uint32_t t2 = (uint32_t)__shfl((int)ctr2, target), t3 = (uint32_t)__shfl((int)ctr3, target);
         double tl[3];
@@ -1408,14 +1433,13 @@ __device__ __forceinline__ int sample_joints_wave(const ctr_system_t &sy, uint64
         const uint64_t acc = __ballot(ok);
         if (unresolved) {
             const int rank = __popcll(m & ((1ull << lane) - 1ull));
-            uint64_t mine = 0;                            // this lane's helpers: rank, rank + cnt, ...
-            for (int i = rank; i < 64; i += cnt) mine |= 1ull << i;
+            const uint64_t mine = c_sample_tabs.stride[cnt] << rank;   // this lane's helpers: rank, rank + cnt, ...
             const uint64_t hit = acc & mine;
             if (hit) {
-                answer = next + (uint32_t)((__builtin_ctzll(hit) - rank) / cnt);
+                answer = next + ((uint32_t)(__builtin_ctzll(hit) - rank) * dv >> 16);
                 unresolved = false;
             } else {
-                next += (uint32_t)((64 - rank + cnt - 1) / cnt);
+                next += (uint32_t)(64 - rank + cnt - 1) * dv >> 16;
             }
         }
     }

@@ -1021,6 +1021,11 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     __shared__ int64_t s_count, s_carried;
     __shared__ int s_par, s_budget;
     __shared__ int32_t s_pref[CARRY_SUBS + 1];           // sub-list starts of the list read
+    // the table inputs' loads first (stage_load), the queue and list counts behind them: one
+    // latency for both before the staging stores them
+    StageRegs stg;
+    stage_load(kc, stg);
+    __builtin_amdgcn_sched_barrier(0);
     CarryHdr *ch = static_cast<CarryHdr *>(b.carry);
     const bool carry_on = RESUMABLE && ch != nullptr && b.carry_cap >= CARRY_SUBS;
     const int64_t sub_cap = b.carry_cap / CARRY_SUBS;
@@ -1036,7 +1041,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     }
     if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
     // (the rigid model's FK never reads the segment LUT: no staging of it)
-    stage_systems<(MODE & 4) == 0>(kc, s_sys, s_raw);
+    stage_systems<(MODE & 4) == 0>(kc, s_sys, s_raw, &stg);
     if (threadIdx.x < 64) {                               // wave 0: prefix sums of the counts read
         int32_t incl = (int32_t)min((int64_t)__shfl(cnt_l, par_l * CARRY_SUBS + (int)(threadIdx.x % CARRY_SUBS)), sub_cap);
         if (threadIdx.x >= CARRY_SUBS) incl = 0;
@@ -1089,7 +1094,10 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             const int64_t ps = queued ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
             // only the resets the env can still take from its ring (see below)
             const bool fresh = queued && b.pool_r[ps] != r && r - (uint32_t)b.epoch[e] - 1u < (uint32_t)b.pool_depth;
-            const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, fresh, odd, (uint64_t)(b.env_base + e), r, nullptr,
+            // every queued entry draws and integrates (a reset is a pure function of (seed, env,
+            // r): an entry that is not fresh computes what it would discard), so the pool_r /
+            // epoch loads behind `fresh` overlap the sampling instead of preceding it
+            const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, queued, odd, (uint64_t)(b.env_base + e), r, nullptr,
                                                    nullptr, -1);
             if (fresh && RL::writer()) {
                 #pragma unroll
@@ -1129,11 +1137,14 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         const uint32_t lead = (queued || carried) ? r - (uint32_t)b.epoch[e] - 1u : 0u;   // resets before r
         const bool fresh = queued && b.pool_r[ps] != r && lead < (uint32_t)b.pool_depth;
         const uint64_t genv = (uint64_t)(b.env_base + e);
-        const int s = fresh ? sample_system(kc.c.seed, r, genv, kc.c.n_systems) : (carried ? rin->sys : 0);
+        // every queued entry draws (draws are a pure function of (seed, env, r); one that is not
+        // fresh discards its joints), so the pool_r / epoch loads behind `fresh` overlap the
+        // sampling instead of preceding it
+        const int s = queued ? sample_system(kc.c.seed, r, genv, kc.c.n_systems) : (carried ? rin->sys : 0);
         float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         uint32_t stat = 0;
         // the wave's new resets draw together (sample_joints_wave): every lane calls it
-        if (sample_joints_wave(s_sys[s], kc.c.seed, r, odd ? 1u : 0u, genv, fresh, qv) > 1000)
+        if (sample_joints_wave(s_sys[s], kc.c.seed, r, odd ? 1u : 0u, genv, queued, qv) > 1000)
             stat |= CTR_STATUS_SAMPLER_STUCK;
         stat |= __shfl_xor(stat, 1);                      // the pair's sampling status
         bool had = false;                                 // this lane's FK finished in an earlier refill

@@ -42,31 +42,29 @@ sub("            fst = st.status;\n        }\n        const bool active = fresh 
 sub("    // the last workgroup to finish clears the queue and the list it read",
     "    DIAG(5);\n    // the last workgroup to finish clears the queue and the list it read")
 # k_step (the compliant one-env-per-lane path): stamps after the array's first half
-sub("    stage_systems<!GROUP>(kc, s_sys, s_raw);\n",
+sub("    StageRegs stg;\n",
     "    unsigned long long *dgp = b.carry ? *reinterpret_cast<unsigned long long *const *>("
     "reinterpret_cast<const char *>(b.carry) + 264) : nullptr;\n"
-    "    if (dgp) dgp += 1024 * 8 * 64;\n    DIAG(0);\n"
-    "    stage_systems<!GROUP>(kc, s_sys, s_raw);\n    DIAG(1);\n")
-sub("        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);\n        FkStats st",
-    "        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a);\n        DIAG(2);\n        FkStats st")
-sub("        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);\n"
-    "        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);\n",
-    "        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, b.epoch[e], (uint64_t)(b.env_base + e)), q, ag, st);\n"
-    "        DIAG(3);\n"
-    "        step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp);\n        DIAG(4);\n")
+    "    if (dgp) dgp += 1024 * 8 * 64;\n    DIAG(0);\n    StageRegs stg;\n")
+sub("    stage_systems<!GROUP>(kc, s_sys, s_raw, &stg);\n",
+    "    stage_systems<!GROUP>(kc, s_sys, s_raw, &stg, dgp);\n    DIAG(1);\n")
+sub("        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);\n        FkStats st",
+    "        set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);\n        DIAG(2);\n        FkStats st")
+sub("        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e)), q, ag, st);\n",
+    "        fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e)), q, ag, st);\n"
+    "        DIAG(3);\n")
+sub("                    s_fin_ep[threadIdx.x], dg_f);\n",
+    "                    s_fin_ep[threadIdx.x], dg_f);\n        DIAG(4);\n")
 # k_step's end, after the refill-queue append (slot 7)
 sub("            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);\n        }\n    }\n}",
     "            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);\n        }\n    }\n    DIAG(7);\n}")
 # staging sub-phases in k_step (slots 5: tables copied + barrier, 6: SysK derived + barrier)
-sub("__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr)\n{",
-    "__device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr,\n"
-    "                                              unsigned long long *dgp = nullptr)\n{")
-sub("            reinterpret_cast<double *>(raw_lds)[i] = rs[i];\n    }\n    __syncthreads();\n",
-    "            reinterpret_cast<double *>(raw_lds)[i] = rs[i];\n    }\n    __syncthreads();\n    DIAG(5);\n")
+sub("                                              const StageRegs *pre = nullptr)\n{",
+    "                                              const StageRegs *pre = nullptr, unsigned long long *dgp = nullptr)\n{")
+sub("                reinterpret_cast<double *>(raw_lds)[i] = rs[i];\n        }\n    }\n    __syncthreads();\n",
+    "                reinterpret_cast<double *>(raw_lds)[i] = rs[i];\n        }\n    }\n    __syncthreads();\n    DIAG(5);\n")
 sub("        __syncthreads();\n        return;\n    }\n    __syncthreads();\n",
     "        __syncthreads();\n        return;\n    }\n    __syncthreads();\n    DIAG(6);\n")
-sub("    stage_systems<!GROUP>(kc, s_sys, s_raw);\n    DIAG(1);\n",
-    "    stage_systems<!GROUP>(kc, s_sys, s_raw, dgp);\n    DIAG(1);\n")
 open(p, "w").write(s)
 EOF
 if [ "${ASM:-0}" = 1 ]; then
