@@ -54,10 +54,16 @@ int hip_check(const char *what)
     return 0;
 }
 
-// Kernel-argument copy of the config (by value, <= 1.2 KB of kernarg).
+// Kernel-argument copy of the config (by value, ~2.7 KB of kernarg).
+// sysk: every system's SysK divisions (kz[3], inv[8], sysk_derive's arithmetic, correctly rounded
+// IEEE divisions and sums, so host and device give the same bits), computed once by make_kcfg
+// on the host: the workgroups copy them with the system rows instead of deriving them behind a
+// barrier of their own.
+constexpr int SYSK_ND = (int)(sizeof(ctr_system_t) / sizeof(double)) + 11;   // rows + kz + inv
 struct KCfg {
     ctr_env_config_t c;
     int32_t mode;       // fk_dispatch MODE bits
+    double sysk[CTR_MAX_SYSTEMS][11];
 };
 
 // LUT = false: skip the per-description segment table (SysK::lut stays NULL; seg_par_at then
@@ -71,14 +77,24 @@ struct StageRegs {
     double sys, raw;
 };
 
-__device__ __forceinline__ void stage_load(const KCfg &kc, StageRegs &r)
+static_assert(offsetof(SysK, kz) == sizeof(ctr_system_t) && offsetof(SysK, inv) == offsetof(SysK, kz) + 3 * sizeof(double),
+              "SysK: the rows, kz and inv contiguous (one copy image)");
+
+// Element k of system s's SysK image (the table row, then kz and inv from the kernel config).
+__device__ __forceinline__ double sysk_elem(const KCfg &kc, int s, int k)
 {
     constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
+    return k < ND ? reinterpret_cast<const double *>(&kc.c.systems[s])[k] : kc.sysk[s][k - ND];
+}
+
+__device__ __forceinline__ void stage_load(const KCfg &kc, StageRegs &r)
+{
     constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
-    static_assert(CTR_MAX_SYSTEMS * ND <= BLOCK && CTR_MAX_SYSTEMS * NR <= BLOCK, "one element per lane");
+    static_assert(CTR_MAX_SYSTEMS * SYSK_ND <= BLOCK && CTR_MAX_SYSTEMS * NR <= BLOCK, "one element per lane");
     trig_table_load(r.trig);
     const int i = (int)threadIdx.x;
-    r.sys = reinterpret_cast<const double *>(kc.c.systems)[i < kc.c.n_systems * ND ? i : 0];
+    const int j = i < kc.c.n_systems * SYSK_ND ? i : 0;
+    r.sys = sysk_elem(kc, j / SYSK_ND, j % SYSK_ND);
     r.raw = reinterpret_cast<const double *>(kc.c.raw)[i < kc.c.n_systems * NR ? i : 0];
 }
 
@@ -87,23 +103,22 @@ template <bool LUT = true>
 __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tube_raw_t *raw_lds = nullptr,
                                               const StageRegs *pre = nullptr)
 {
-    constexpr int ND = (int)(sizeof(ctr_system_t) / sizeof(double));
     constexpr int NR = (int)(sizeof(ctr_tube_raw_t) / sizeof(double));
-    const double *src = reinterpret_cast<const double *>(kc.c.systems);
-    const int nd = kc.c.n_systems * ND;
+    // seg_par of every (system, 6-bit gap description): SysK::lut, read at segment starts
+    __shared__ double s_lut[CTR_MAX_SYSTEMS][64][8];
+    const int nd = kc.c.n_systems * SYSK_ND;
     if (pre) {
         // unconditional stores (lanes past the rows write a dummy slot): a conditional store would
         // let the compiler sink its load behind the caller's loads
         __shared__ double s_stage_dummy[BLOCK];
         const int i = (int)threadIdx.x;
-        double *ds = i < nd ? reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND])) + i % ND
-                            : &s_stage_dummy[i];
+        double *ds = i < nd ? reinterpret_cast<double *>(&lds[i / SYSK_ND]) + i % SYSK_ND : &s_stage_dummy[i];
         *ds = pre->sys;
         trig_table_store(pre->trig);
         if (raw_lds) *(i < kc.c.n_systems * NR ? reinterpret_cast<double *>(raw_lds) + i : &s_stage_dummy[i]) = pre->raw;
     } else {
         for (int i = threadIdx.x; i < nd; i += blockDim.x)
-            reinterpret_cast<double *>(static_cast<ctr_system_t *>(&lds[i / ND]))[i % ND] = src[i];
+            reinterpret_cast<double *>(&lds[i / SYSK_ND])[i % SYSK_ND] = sysk_elem(kc, i / SYSK_ND, i % SYSK_ND);
         trig_table_fill();
         if (raw_lds) {
             const double *rs = reinterpret_cast<const double *>(kc.c.raw);
@@ -111,25 +126,30 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tub
                 reinterpret_cast<double *>(raw_lds)[i] = rs[i];
         }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kc.c.n_systems * 11; i += blockDim.x) sysk_derive(lds[i / 11], i % 11);
-    if (!LUT) {
-        for (int i = threadIdx.x; i < kc.c.n_systems; i += blockDim.x) lds[i].lut = nullptr;
-        __syncthreads();
-        return;
+    for (int i = threadIdx.x; i < kc.c.n_systems; i += blockDim.x) lds[i].lut = LUT ? &s_lut[i][0][0] : nullptr;
+    if (LUT) {
+        // the table rows from the kernel config (wave-uniform system: scalar loads), not from the
+        // LDS copy above, so the workgroup needs one barrier for both
+        for (int i = threadIdx.x; i < kc.c.n_systems * 64; i += blockDim.x) {
+            const int sy = i / 64;
+            SysK t;
+            #pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                t.EI[j] = kc.c.systems[sy].EI[j];
+                t.Ux[j] = kc.c.systems[sy].Ux[j];
+                t.Uy[j] = kc.c.systems[sy].Uy[j];
+                t.kz[j] = kc.sysk[sy][j];
+            }
+            #pragma unroll
+            for (int m = 0; m < 8; ++m) t.inv[m] = kc.sysk[sy][3 + m];
+            SegPar q = seg_par(t, (uint32_t)(i % 64), false);
+            seg_fold_inv(q);
+            double *e = s_lut[sy][i % 64];
+            for (int j = 0; j < 3; ++j) { e[j] = q.wx[j]; e[3 + j] = q.g[j]; }
+            e[6] = q.inv;
+            e[7] = (double)q.present;
+        }
     }
-    __syncthreads();
-    // seg_par of every (system, 6-bit gap description): SysK::lut, read at segment starts
-    __shared__ double s_lut[CTR_MAX_SYSTEMS][64][8];
-    for (int i = threadIdx.x; i < kc.c.n_systems * 64; i += blockDim.x) {
-        SegPar q = seg_par(lds[i / 64], (uint32_t)(i % 64), false);
-        seg_fold_inv(q);
-        double *e = s_lut[i / 64][i % 64];
-        for (int j = 0; j < 3; ++j) { e[j] = q.wx[j]; e[3 + j] = q.g[j]; }
-        e[6] = q.inv;
-        e[7] = (double)q.present;
-    }
-    for (int i = threadIdx.x; i < kc.c.n_systems; i += blockDim.x) lds[i].lut = &s_lut[i][0][0];
     __syncthreads();
 }
 
@@ -1336,6 +1356,17 @@ KCfg make_kcfg(const ctr_env_config_t *cfg)
 {
     KCfg kc;
     memcpy(&kc.c, cfg, sizeof *cfg);
+    memset(kc.sysk, 0, sizeof kc.sysk);
+    for (int s = 0; s < cfg->n_systems && s < CTR_MAX_SYSTEMS; ++s) {
+        // sysk_derive's arithmetic (kz_j = EI_j / GJ_j, model.py:97; inv[m] = 1 / sum of the EI
+        // present in mask m, model.py:83): one correctly rounded operation at a time
+        const ctr_system_t &y = cfg->systems[s];
+        for (int j = 0; j < 3; ++j) kc.sysk[s][j] = y.EI[j] / y.GJ[j];
+        for (int m = 0; m < 8; ++m) {
+            const double e0 = (m & 1) ? y.EI[0] : 0.0, e1 = (m & 2) ? y.EI[1] : 0.0, e2 = (m & 4) ? y.EI[2] : 0.0;
+            kc.sysk[s][3 + m] = 1.0 / ((e0 + e1) + e2);
+        }
+    }
     int has_uy = 0;
     for (int s = 0; s < cfg->n_systems; ++s)
         for (int i = 0; i < 3; ++i)

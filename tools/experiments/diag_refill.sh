@@ -61,10 +61,9 @@ sub("            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, tw
 # staging sub-phases in k_step (slots 5: tables copied + barrier, 6: SysK derived + barrier)
 sub("                                              const StageRegs *pre = nullptr)\n{",
     "                                              const StageRegs *pre = nullptr, unsigned long long *dgp = nullptr)\n{")
-sub("                reinterpret_cast<double *>(raw_lds)[i] = rs[i];\n        }\n    }\n    __syncthreads();\n",
-    "                reinterpret_cast<double *>(raw_lds)[i] = rs[i];\n        }\n    }\n    __syncthreads();\n    DIAG(5);\n")
-sub("        __syncthreads();\n        return;\n    }\n    __syncthreads();\n",
-    "        __syncthreads();\n        return;\n    }\n    __syncthreads();\n    DIAG(6);\n")
+# (one barrier since the SysK divisions come from the kernel config: slot 6 = slot 5)
+sub("            e[7] = (double)q.present;\n        }\n    }\n    __syncthreads();\n",
+    "            e[7] = (double)q.present;\n        }\n    }\n    __syncthreads();\n    DIAG(5);\n    DIAG(6);\n")
 open(p, "w").write(s)
 EOF
 if [ "${ASM:-0}" = 1 ]; then
