@@ -93,3 +93,18 @@ def test_inv_root10_and_sqrt(tmp_path):
     s = np.empty_like(xs)
     lib.vsqrt(xs.ctypes.data, s.ctypes.data, len(xs))
     assert _ulp_err(s, np.sqrt(xs)).max() <= 2.0
+
+
+def test_sampler_round_tables():
+    """The wave sampler's per-round constants (ctr_device.hpp SampleTabs): for k = 1..64 unresolved
+    lanes, x // k == (x * ceil(2^16 / k)) >> 16 for every 0 <= x <= 128 (the sampler divides
+    lane, ctz(hit) - rank <= 63 and 64 - rank + k - 1 <= 127 by k), and stride[k] << rank is the
+    set {rank, rank + k, ...} below 64 that the former loop built."""
+    for k in range(1, 65):
+        m = -(-65536 // k)
+        for x in range(129):
+            assert (x * m) >> 16 == x // k, (k, x)
+        stride = sum(1 << i for i in range(0, 64, k))
+        for rank in range(k):
+            want = sum(1 << i for i in range(rank, 64, k))
+            assert (stride << rank) & ((1 << 64) - 1) == want, (k, rank)
