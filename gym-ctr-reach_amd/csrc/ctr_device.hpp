@@ -1383,7 +1383,7 @@ constexpr SampleTabs make_sample_tabs()
     }
     return t;
 }
-__constant__ SampleTabs c_sample_tabs = make_sample_tabs();
+static __constant__ SampleTabs c_sample_tabs = make_sample_tabs();   // internal linkage: the header may enter several translation units
 
 __device__ __forceinline__ int sample_joints_wave(const ctr_system_t &sy, uint64_t seed, uint32_t epoch,
                                                   uint32_t stream, uint64_t env, bool need, float q[6])
