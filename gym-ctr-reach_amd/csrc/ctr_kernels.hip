@@ -985,9 +985,9 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
 // suspended.  Refill k reads list `parity` (resuming every reset on it) and appends to the other;
 // its last workgroup empties the list it read and flips `parity`, so HIP-graph replays of the
 // refill alternate the lists without host involvement.  Each list is CARRY_SUBS sub-lists with
-// their own counters (workgroup b appends to sub-list b mod CARRY_SUBS): the waves of a refill
+// their own counters (workgroup b appends to sub-list b mod nsub, nsub = min(CARRY_SUBS, grid)): the waves of a refill
 // all suspend at about the same time, and one counter for all 1 024 of them serialised their
-// atomics (~7 us of the refill's tail, clock-stamped build).
+// atomics (~7 us of the refill's tail, clock-stamped build); 64 sub-lists put 16 waves on each.
 struct CarryRec {
     FkSuspend fk[2];          // the suspended goal FK (even lane) / start FK (odd lane)
     double tip[2][3];         // the tip of an FK that has finished
@@ -1002,14 +1002,14 @@ struct CarryRec {
 };
 static_assert(sizeof(CarryRec) == 640, "CarryRec layout");
 
-constexpr int CARRY_SUBS = 32;
+constexpr int CARRY_SUBS = 64;
 
 struct CarryHdr {
     int32_t count[2][CARRY_SUBS];   // resets on each sub-list of each list
     int32_t parity;                 // the list the next refill reads
-    int32_t pad[63];
+    int32_t pad[127];
 };
-static_assert(sizeof(CarryHdr) == 512, "CarryHdr layout");
+static_assert(sizeof(CarryHdr) == 1024, "CarryHdr layout");
 
 // One FK of a refill: the scipy-RK45 FK runs at most `budget` iterations and can start from a
 // suspended state (fk_lane RESUME); fixed-step RK4 always runs to the end.
@@ -1047,24 +1047,27 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
     stage_load(kc, stg);
     __builtin_amdgcn_sched_barrier(0);
     CarryHdr *ch = static_cast<CarryHdr *>(b.carry);
-    const bool carry_on = RESUMABLE && ch != nullptr && b.carry_cap >= CARRY_SUBS;
-    const int64_t sub_cap = b.carry_cap / CARRY_SUBS;
+    // sub-lists in use: one per dealing workgroup up to CARRY_SUBS (the grid is the same every
+    // refill of a batch, so writer and reader agree), each carry_cap / nsub records long
+    const int nsub = (int)min((int64_t)CARRY_SUBS, min((int64_t)gridDim.x, (int64_t)256));
+    const bool carry_on = RESUMABLE && ch != nullptr && b.carry_cap >= nsub;
+    const int64_t sub_cap = b.carry_cap / nsub;
     // the list's parity and sub-list counts: loaded by wave 0 now, used after the staging below
     // (its barriers do not wait for them)
     // (both lists' counts: no load waits for the parity)
-    static_assert(2 * CARRY_SUBS == 64, "one count per lane of wave 0");
+    static_assert(CARRY_SUBS == 64, "one count of each list per lane of wave 0");
     int par_l = 0;
-    int32_t cnt_l = 0;
+    int32_t cnt_a = 0, cnt_b = 0;
     if (threadIdx.x < 64 && carry_on) {
         par_l = ch->parity & 1;
-        cnt_l = ch->count[threadIdx.x / CARRY_SUBS][threadIdx.x % CARRY_SUBS];
+        cnt_a = ch->count[0][threadIdx.x];
+        cnt_b = ch->count[1][threadIdx.x];
     }
     if (threadIdx.x == 0) s_count = min((int64_t)b.refill[0], b.refill_cap);
     // (the rigid model's FK never reads the segment LUT: no staging of it)
     stage_systems<(MODE & 4) == 0>(kc, s_sys, s_raw, &stg);
     if (threadIdx.x < 64) {                               // wave 0: prefix sums of the counts read
-        int32_t incl = (int32_t)min((int64_t)__shfl(cnt_l, par_l * CARRY_SUBS + (int)(threadIdx.x % CARRY_SUBS)), sub_cap);
-        if (threadIdx.x >= CARRY_SUBS) incl = 0;
+        int32_t incl = (int32_t)min((int64_t)(par_l ? cnt_b : cnt_a), sub_cap);
         #pragma unroll
         for (int off = 1; off < CARRY_SUBS; off <<= 1) {
             const int32_t v = __shfl_up(incl, off);
@@ -1081,7 +1084,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             const int64_t G = min((int64_t)gridDim.x, (int64_t)256);
             const int64_t per_pass = G * (BLOCK / 64) * 32;
             const int64_t passes = (s_count + incl + per_pass - 1) / per_pass;
-            const int64_t inflow = (G + CARRY_SUBS - 1) / CARRY_SUBS * (BLOCK / 64) * 32 * passes;
+            const int64_t inflow = (G + nsub - 1) / nsub * (BLOCK / 64) * 32 * passes;
             s_budget = (carry_on && b.refill_budget > 0 && inflow <= sub_cap) ? b.refill_budget : 0;
         }
     }
@@ -1216,7 +1219,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             if (m) {
                 const int leader = __builtin_ctzll(m);
                 int slot = 0;
-                const int sub = blockIdx.x % CARRY_SUBS;
+                const int sub = blockIdx.x % nsub;
                 if (lane == leader) slot = atomicAdd(&ch->count[par ^ 1][sub], __popcll(m));
                 slot = __shfl(slot, leader) + __popcll(m & ((1ull << (lane | 1)) - 1ull));
                 if (keep && slot < sub_cap) {

@@ -299,7 +299,7 @@ class CtrReachVecEnv(object):
         """Resets on the two suspended lists (resumable refill; diagnostics, synchronises)."""
         if self.carry is None:
             return (0, 0)
-        c = self.carry[:256].view(_torch().int32).view(2, 32).sum(dim=1).tolist()   # CarryHdr.count[2][32]
+        c = self.carry[:512].view(_torch().int32).view(2, 64).sum(dim=1).tolist()   # CarryHdr.count[2][64]
         return (c[0], c[1])
 
     def refill_pool(self, stream=None):

@@ -367,7 +367,7 @@ int ctr_reset(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const uint8
 int ctr_pool_refill(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
 
 /* Bytes of batch->carry for carry_cap resets per list (a header, then two lists of suspended
- * resets, each in 32 sub-lists); int32 counts[2][32] at byte 0 of the header give the resets each
+ * resets, each in 64 sub-lists); int32 counts[2][64] at byte 0 of the header give the resets each
  * sub-list holds (diagnostics). */
 int64_t ctr_refill_carry_bytes(int64_t carry_cap);
 

@@ -30,12 +30,12 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_refill_carry_bytes():
-    """ctr_refill_carry_bytes (host arithmetic, no GPU): a 512-B header (counts[2][32], parity),
+    """ctr_refill_carry_bytes (host arithmetic, no GPU): a 1-KB header (counts[2][64], parity),
     then two lists of 640-B suspended-reset records; negative capacities give 0."""
     from ctr_reach_amd import _abi
     lib = _abi.load()
     for cap in (0, 1, 256, 131072):
-        assert lib.ctr_refill_carry_bytes(cap) == 512 + 2 * cap * 640
+        assert lib.ctr_refill_carry_bytes(cap) == 1024 + 2 * cap * 640
     assert lib.ctr_refill_carry_bytes(-5) == 0
 
 

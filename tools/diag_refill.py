@@ -36,7 +36,7 @@ env._steps_since_refill = 0
 env.step_raw(acts[0])
 torch.cuda.synchronize()
 stamps = torch.zeros(2 * 1024 * 8 * 64, dtype=torch.int64, device="cuda")
-env.carry[264:272].copy_(torch.tensor([stamps.data_ptr()], dtype=torch.int64).view(torch.uint8))
+env.carry[520:528].copy_(torch.tensor([stamps.data_ptr()], dtype=torch.int64).view(torch.uint8))
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 torch.cuda._sleep(200000)
 e0.record()

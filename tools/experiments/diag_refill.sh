@@ -26,11 +26,11 @@ sub("constexpr int BLOCK = 256;",
     "#define DIAG(ph) do { const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); "
     "if (dgp && blockIdx.x < 256) "
     "dgp[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (ph)) * 64 + (threadIdx.x & 63)] = _t; } while (0)")
-# the stamp array's address: bytes 264..271 of the carry header (its padding), set by the host tool
-sub("    CarryHdr *ch = static_cast<CarryHdr *>(b.carry);\n    const bool carry_on = RESUMABLE",
+# the stamp array's address: bytes 520..527 of the carry header (its padding), set by the host tool
+sub("    CarryHdr *ch = static_cast<CarryHdr *>(b.carry);\n",
     "    CarryHdr *ch = static_cast<CarryHdr *>(b.carry);\n"
-    "    unsigned long long *dgp = ch ? *reinterpret_cast<unsigned long long *const *>(reinterpret_cast<const char *>(ch) + 264) : nullptr;\n"
-    "    DIAG(0);\n    const bool carry_on = RESUMABLE")
+    "    unsigned long long *dgp = ch ? *reinterpret_cast<unsigned long long *const *>(reinterpret_cast<const char *>(ch) + 520) : nullptr;\n"
+    "    DIAG(0);\n")
 sub("    __syncthreads();\n    CarryRec *recs",
     "    __syncthreads();\n    DIAG(1);\n    CarryRec *recs")
 sub("            stat |= CTR_STATUS_SAMPLER_STUCK;\n        stat |= __shfl_xor(stat, 1);",
@@ -44,7 +44,7 @@ sub("    // the last workgroup to finish clears the queue and the list it read",
 # k_step (the compliant one-env-per-lane path): stamps after the array's first half
 sub("    StageRegs stg;\n",
     "    unsigned long long *dgp = b.carry ? *reinterpret_cast<unsigned long long *const *>("
-    "reinterpret_cast<const char *>(b.carry) + 264) : nullptr;\n"
+    "reinterpret_cast<const char *>(b.carry) + 520) : nullptr;\n"
     "    if (dgp) dgp += 1024 * 8 * 64;\n    DIAG(0);\n    StageRegs stg;\n")
 sub("    stage_systems<!GROUP>(kc, s_sys, s_raw, &stg);\n",
     "    stage_systems<!GROUP>(kc, s_sys, s_raw, &stg, dgp);\n    DIAG(1);\n")
