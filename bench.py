@@ -19,10 +19,14 @@ anything touches a GPU); under ``torch.distributed.run`` the ranks come from the
 Rank r owns the contiguous global env ids [r n, (r + 1) n) (weak scaling, no collective on the
 step itself).  With N > 1 every timed step also all-gathers the packed step outputs (16 B/env:
 tip, done | success | reward) -- BASELINE configs[3] -- while the next step runs; k_step writes
-the packed rows itself (pack_outputs).  Default gather: the fused push (--gather-backend push,
-distributed.PushGather): k_step itself stores every env's row into every rank's IPC-mapped
-receive ring, with no extra launch; RCCL's kernels hold CUs the next step needs.  A
-barrier + device sync bracket the timed region and the time is the MAX over ranks.
+the packed rows itself (pack_outputs).  Default gather (--gather-backend auto): the fused push
+(distributed.PushGather: k_step itself stores every env's row into every rank's IPC-mapped
+receive ring, paced by the ranks' slot releases, and waits until every rank's rows of the previous
+step are in its own ring), checked bit for bit against a process-group all_gather on every step
+of two refill periods before any timing, then timed against RCCL (whose kernels hold CUs the next
+step needs); a failed check sends every rank to RCCL, and a failed check after the
+window exits non-zero without a line.  A barrier + device sync bracket the timed region and the
+time is the MAX over ranks.
 
 Also reported: the dominant kernel's roofline (algorithmic FP64 flops / its average launch
 time measured with HIP events on the launch stream) and the CPU oracle timed on this host
@@ -358,7 +362,13 @@ def main():
         backend_used = args.gather_backend
         if backend_used in ("push", "sdma", "auto"):
             try:
-                env.enable_gather("sdma" if backend_used == "sdma" else "push")
+                # push: depth 3 and the fused consumer wait (k_step(t) returns only once every
+                # rank's rows of step t - 1 are in this rank's ring), so every timed step also
+                # completes a gather, as RCCL's stream-ordered collective does
+                if backend_used == "sdma":
+                    env.enable_gather("sdma")
+                else:
+                    env.enable_gather("push", depth=3, wait_prev=True)
             except Exception as ex:          # noqa: BLE001 -- reported in the line, RCCL measured instead
                 print("bench.py: %s gather setup failed (%s); using rccl" % (backend_used, ex), file=sys.stderr,
                       flush=True)
@@ -418,6 +428,22 @@ def main():
     gc.collect()
     gc.disable()
     done_pre = 0
+    check = None
+    if backend_used in ("push", "auto"):
+        # before any timing: every push step of 2 refill periods waited on and bit-compared, on
+        # every rank, with a process-group all_gather of the ranks' own rows (the reference copy);
+        # a mismatch or a wait error on any rank sends every rank to RCCL, with the reason
+        def push_step(i):
+            one_step(done_pre + i)
+            return env.gather_seq
+        check = D.check_push_steps(push_step, push_gather, env.packed_outputs, 2 * R,
+                                   stream=torch.cuda.current_stream())
+        done_pre += check["steps_checked"]
+        if not check["passed"]:
+            print("bench.py: push gather check failed (%s); using rccl" % check, file=sys.stderr, flush=True)
+            fallback_note = "push gather check failed: %s" % json.dumps(check)
+            backend_used = state["mode"] = "rccl"
+            env._push_gather = None
     if backend_used == "auto":
         # pick the faster gather on this node: 2 refill periods of each (untimed, max over ranks);
         # the push stores ride inside the steps, so RCCL's turn runs with the push detached
@@ -431,7 +457,8 @@ def main():
         backend_used = min(("push", "rccl"), key=lambda m: calibration[m + "_ms_per_step"])
         state["mode"] = backend_used
         env._push_gather = push_gather if backend_used == "push" else None
-        pre = max(pre, done_pre + R)
+    # the window starts on a refill boundary: whole refill periods before it
+    pre = max(pre, -(-(done_pre + R) // R) * R)
     for i in range(done_pre, pre):
         one_step(i)
     use_graph = args.graph == "on" or (args.graph == "auto" and not gather)
@@ -480,22 +507,21 @@ def main():
     if backend_used in ("push", "sdma"):
         # the window's last gather, checked where it landed: this rank's slot holds every rank's
         # rows of the last timed step (consumer wait, then a bit-exact compare with the gloo/RCCL
-        # copy of the same rows); outside the timed region
+        # copy of the same rows), and no rank's error word has a bit set (a wait or a slot
+        # release that timed out in any step of the window); outside the timed region
         seq = env.gather_seq if backend_used == "push" else env.packed_seq
-        mine = env.packed_outputs().clone()
-        out = env._push_gather.wait(seq, torch.cuda.current_stream())
-        blocks = [torch.empty_like(mine) for _ in range(ws)]
-        if backend == "gloo":
-            hb = [b.cpu() for b in blocks]
-            dist.all_gather(hb, mine.cpu())
-            blocks = [b.to(dev) for b in hb]
-        else:
-            dist.all_gather(blocks, mine)
-        torch.cuda.synchronize()
-        gather_check = {"last_step_rows_equal": bool(torch.equal(out, torch.cat(blocks))),
-                        "wait_error": int(env._push_gather.err.item())}
+        ok, rep = D.verify_gathered(env._push_gather.wait(seq, torch.cuda.current_stream()), env.packed_outputs(),
+                                    env._push_gather.err, group=None)
+        gather_check = dict(rep, last_step_rows_equal=rep["rows_equal_all_ranks"], passed=ok)
+        if not ok:
+            # a fast, wrong headline is worse than none: no line, non-zero exit on every rank
+            print("bench.py: the %s gather of the window failed its check: %s" % (backend_used, json.dumps(rep)),
+                  file=sys.stderr, flush=True)
+            if dist:
+                dist.destroy_process_group()
+            return 3
     el = D.max_over_ranks(el_local, device=dev if backend in (None, "nccl") else "cpu")
-    traffic, traffic_note = measured_traffic(n, cfgd, systems)
+    traffic, traffic_note = measured_traffic(n, cfgd, systems) if ws == 1 else (None, None)
     resets_local = int((env.epoch.to(torch.int64).sum() - epoch0).item())
     refills = env.refills - refills0
     sweeps = env.sweeps - sweeps0
@@ -556,8 +582,17 @@ def main():
                    "envs_per_gpu": n, "global_envs": n * ws, "parallelism": "env-shard x%d" % ws,
                    "process_group": {"backend": backend, "world_size": ws} if dist else None,
                    "all_gather": dict({"bytes_per_env": 4 * D.PACK_WIDTH, "async": True, "backend": backend_used},
-                                      **({"engine": env._push_gather.engine, "check": gather_check}
+                                      **({"engine": env._push_gather.engine, "depth": env._push_gather.depth,
+                                          "consumer_wait": "fused: k_step(t) completes once every rank's rows of "
+                                                           "step t - 1 are in this rank's ring"
+                                          if env._push_gather.wait_prev else "none in the window",
+                                          "check": gather_check}
                                          if backend_used in ("push", "sdma") else {}),
+                                      **({"pre_window_check": check} if check else {}),
+                                      **({"rccl_channels": "RCCL's own choice (uncapped): on one GPU an RCCL-footprint "
+                                                           "gather costs its duration + ~7 us whatever its workgroup "
+                                                           "count, so a channel cap only lengthens it (DESIGN.md 6.2)"}
+                                         if backend_used == "rccl" else {}),
                                       **({"calibration": calibration, "chosen_by": "calibration"}
                                          if calibration else {}),
                                       **({"fallback": fallback_note} if fallback_note else {}))
@@ -592,7 +627,13 @@ def main():
                                if cfgd["model"] == "rigid" else "SURVEY 8(d) count"))},
     }
     tr = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tr):
+    if ws > 1:
+        # the one-GPU PMC passes do not see a rank's stores into its peers' rings (16 B per env and
+        # peer) nor RCCL's traffic
+        out["roofline"]["traffic"] = None
+        out["roofline"]["traffic_source"] = ("not measured for N > 1: profiles/traffic.json is k_step on one GPU "
+                                             "without the gather's peer stores")
+    elif os.path.exists(tr):
         with open(tr) as fh:
             t = json.load(fh)
         if t.get("envs") == n and t.get("config", 3) == args.config and systems == [0]:

@@ -157,7 +157,9 @@ struct SegPar {
     uint32_t present;  // bit j: tube j present (EI_j != 0)
 };
 
-__device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool rigid = false)
+// inv: 1 / the EI sum of the present tubes, sy.inv[bits6 & 7] (seg_par) -- passed in by a caller
+// whose SysK is a private copy, where that dynamic index would place the copy in scratch memory.
+__device__ __forceinline__ SegPar seg_par_inv(const SysK &sy, uint32_t bits6, bool rigid, double inv)
 {
     SegPar p;
     #pragma unroll
@@ -171,11 +173,16 @@ __device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool r
         p.wy[j] = ei * p.uy0[j];
         p.kz[j] = (pres && !rigid) ? sy.kz[j] : 0.0;   // torsionally rigid: GJ -> infinity
     }
-    p.inv = sy.inv[bits6 & 7u];
+    p.inv = inv;
     #pragma unroll
     for (int j = 0; j < 3; ++j) p.g[j] = (p.kz[j] * p.ux0[j]) * p.inv;
     p.present = (uint32_t)(bits6 & 7u);
     return p;
+}
+
+__device__ __forceinline__ SegPar seg_par(const SysK &sy, uint32_t bits6, bool rigid = false)
+{
+    return seg_par_inv(sy, bits6, rigid, sy.inv[bits6 & 7u]);
 }
 
 // No y pre-curvature: the RHS uses inv only as a factor of every wx product, so fold it in

@@ -140,9 +140,9 @@ __device__ __forceinline__ void stage_systems(const KCfg &kc, SysK *lds, ctr_tub
                 t.Uy[j] = kc.c.systems[sy].Uy[j];
                 t.kz[j] = kc.sysk[sy][j];
             }
-            #pragma unroll
-            for (int m = 0; m < 8; ++m) t.inv[m] = kc.sysk[sy][3 + m];
-            SegPar q = seg_par(t, (uint32_t)(i % 64), false);
+            // inv read by its dynamic index from the kernel config, not from t (a dynamic index
+            // into the private copy put it in scratch: 72 B per lane written back to HBM)
+            SegPar q = seg_par_inv(t, (uint32_t)(i % 64), false, kc.sysk[sy][3 + (i & 7)]);
             seg_fold_inv(q);
             double *e = s_lut[sy][i % 64];
             for (int j = 0; j < 3; ++j) { e[j] = q.wx[j]; e[3 + j] = q.g[j]; }
@@ -245,6 +245,64 @@ __device__ __forceinline__ void gather_publish_lane(const ctr_gather_push_t *g, 
 {
     if ((int)threadIdx.x < g->world)
         __hip_atomic_store(g->seqw[threadIdx.x], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Sequence numbers wrap modulo 2^32: a has reached b.
+__device__ __forceinline__ bool seq_reached(uint32_t a, uint32_t b) { return (int32_t)(a - b) >= 0; }
+
+// Fused push flow control (include/ctr_reach_amd.h, "Push all-gather"): lane k < world stores
+// `released` into this rank's release word in rank k's memory (release, system scope; the
+// launch's stream predecessors, which held this rank's reads of the released slot, are complete).
+__device__ __forceinline__ void gather_release_lane(const ctr_gather_push_t *g, uint32_t released)
+{
+    if ((int)threadIdx.x < g->world)
+        __hip_atomic_store(g->relw[threadIdx.x], released, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// This lane's release word of consumer (lane) -- ~0u for lanes >= world (always free).
+__device__ __forceinline__ uint32_t gather_release_load(const ctr_gather_push_t *g, uint32_t seq)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    return lane < g->world ? __hip_atomic_load(g->rel + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                           : seq - (uint32_t)g->depth;
+}
+
+// Wave-uniform: every consumer has released the slot step seq rewrites (step seq - depth).
+// Call with every lane of the wave active.
+__device__ __forceinline__ bool gather_slot_free(const ctr_gather_push_t *g, uint32_t seq, uint32_t rel)
+{
+    return __ballot(!seq_reached(rel, seq - (uint32_t)g->depth)) == 0;
+}
+
+// Bounded wait (every lane active) for the slot of step seq; false after spin_limit polls.
+__device__ __noinline__ bool gather_wait_slot(const ctr_gather_push_t *g, uint32_t seq)
+{
+    for (uint32_t k = 0;; ++k) {
+        if (gather_slot_free(g, seq, gather_release_load(g, seq))) return true;
+        if (k >= g->spin_limit) return false;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// The fused consumer wait (ctr_step_out_t.gather_wait_prev): lane k < world polls this rank's
+// sequence word of rank k's block of the previous slot until it reaches seq (acquire, system
+// scope); bounded, errors into g->err.
+__device__ __noinline__ void gather_wait_prev_lane(const ctr_gather_push_t *g, uint32_t seq)
+{
+    const int lane = (int)threadIdx.x;
+    if (lane >= g->world) return;
+    for (uint32_t k = 0;; ++k) {
+        const uint32_t v = __hip_atomic_load(g->wait_seqw + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (seq_reached(v, seq)) {
+            if (v != seq) atomicOr(g->err, CTR_GATHER_E_OVERWRITTEN);
+            return;
+        }
+        if (k >= g->spin_limit) {
+            atomicOr(g->err, CTR_GATHER_E_PREV_TIMEOUT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
 }
 
 // Row e of an observation buffer: float32 [n][od] or, with cfg.obs_f64, float64 [n][od].
@@ -465,7 +523,8 @@ struct StepFlags {
 __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o, int64_t e,
                                             int s, float q[6], double ag[3], const FkStats &st, int32_t autoreset,
                                             StepFlags &fl, const ctr_her_t *her, const float *action,
-                                            const PoolPre &pp, int32_t t_prev, uint32_t epoch, const double dg_prev[3])
+                                            const PoolPre &pp, int32_t t_prev, uint32_t epoch, const double dg_prev[3],
+                                            float4 &grow)
 {
     const int32_t t = t_prev + 1;
     double dg[3];
@@ -493,7 +552,7 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
         const float fl = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0) | ((reward < 0.0f) ? 4 : 0));
         const float4 row = make_float4((float)ag[0], (float)ag[1], (float)ag[2], fl);
         if (o.packed) *reinterpret_cast<float4 *>(o.packed + 4 * e) = row;
-        if (o.gather) gather_store_row(o.gather, e, row);      // the fused push gather
+        grow = row;                                             // the fused push (step_body)
     }
     // ctr_step_her: the transition goes into the env's HER episode before any auto-reset
     if (her) {
@@ -569,7 +628,7 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
 __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o,
                                                   int64_t e, int j, bool in, int s, const float q[6], double ag[3],
                                                   const FkStats &st, int32_t autoreset, StepFlags &fl,
-                                                  const PoolPre &pp)
+                                                  const PoolPre &pp, float4 &grow)
 {
     const int lead = (int)(threadIdx.x & 63) & ~(SEG_GROUP - 1);
     #pragma unroll
@@ -611,7 +670,7 @@ __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batc
             const float fl4 = (float)((done ? 1 : 0) | ((d < tol) ? 2 : 0) | ((reward < 0.0f) ? 4 : 0));
             const float4 row = make_float4((float)ag[0], (float)ag[1], (float)ag[2], fl4);
             if (o.packed) *reinterpret_cast<float4 *>(o.packed + 4 * e) = row;
-            if (o.gather) gather_store_row(o.gather, e, row);
+            grow = row;
         }
         uint32_t stat = st.status;
         if (autoreset && done) {
@@ -692,7 +751,11 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     double dg_in[3];
     #pragma unroll
     for (int i = 0; i < 3; ++i) dg_in[i] = b.desired_goal[3 * ec + i];
+    // fused push: the consumers' release words, read behind the staging (checked after it)
+    const ctr_gather_push_t *gp = o.gather;
+    const uint32_t rel0 = gp ? gather_release_load(gp, o.gather_seq) : 0u;
     stage_systems<!GROUP>(kc, s_sys, s_raw, &stg);
+    const bool slot_free0 = gp ? gather_slot_free(gp, o.gather_seq, rel0) : true;
     // one env per lane: the finish's inputs wait out the FK in LDS (they have landed during the
     // staging), not in registers the FK loop would have to keep
     __shared__ double s_fin_dg[3][BLOCK];
@@ -708,9 +771,14 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     if (o.packed && o.packed_seq && blockIdx.x == 0 && threadIdx.x == 0)
         *reinterpret_cast<uint4 *>(o.packed + 4 * b.n) = make_uint4(o.packed_seq, 0u, 0u, 0u);
     // fused push gather: the previous gathered step's launch has completed, so its rows are in
-    // every rank's ring; publish its sequence word there
-    if (o.gather_prev && blockIdx.x == 0) gather_publish_lane(o.gather_prev, o.gather_prev_seq);
+    // every rank's ring (performed at system scope); publish its sequence word there, and release
+    // this rank's slot of step gather_seq + 1 - depth (its readers ran before this launch)
+    if (blockIdx.x == 0) {
+        if (o.gather_prev) gather_publish_lane(o.gather_prev, o.gather_prev_seq);
+        if (gp) gather_release_lane(gp, o.gather_seq + 1u - (uint32_t)gp->depth);
+    }
     StepFlags fl;
+    float4 grow = make_float4(0.f, 0.f, 0.f, 0.f);   // this lane's gather row (fused push)
     if constexpr (GROUP) {
         // every lane of the wave takes part in the group's shuffles
         int s = 0;
@@ -734,9 +802,10 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         else
             fk_group_rigid4<(MODE & 1) != 0, false>(sy, qd, j, ag, st, (double)kc.c.rk4_steps_per_m);
         if constexpr (HER) {
-            if (live) step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, t_in, ep_in, dg_in);
+            if (live)
+                step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, t_in, ep_in, dg_in, grow);
         } else {
-            step_finish_group(kc, b, o, e, j, in, s, q, ag, st, autoreset, fl, pp);
+            step_finish_group(kc, b, o, e, j, in, s, q, ag, st, autoreset, fl, pp, grow);
         }
     } else if (live) {
         const int s = clamp_sys(s_in, kc.c.n_systems);
@@ -754,7 +823,7 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         #pragma unroll
         for (int i = 0; i < 3; ++i) dg_f[i] = s_fin_dg[i][threadIdx.x];
         step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, s_fin_t[threadIdx.x],
-                    s_fin_ep[threadIdx.x], dg_f);
+                    s_fin_ep[threadIdx.x], dg_f, grow);
     }
     if (autoreset) {
         if (autoreset == CTR_AUTORESET_POOLED) {
@@ -769,6 +838,19 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             const int32_t two[2] = {(int32_t)e, (int32_t)(fl.pooled_r + (uint32_t)b.pool_depth)};
             wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
         }
+    }
+    if (gp) {
+        // the fused push (every lane of the wave here): once every consumer has released the
+        // slot (normally known since the staging), each env's row into every rank's ring, then a
+        // system-scope release, so the rows are performed at system scope before the wave ends
+        // and the next launch publishes the sequence words (include/ctr_reach_amd.h)
+        if (!slot_free0 && !gather_wait_slot(gp, o.gather_seq) && (threadIdx.x & 63) == 0)
+            atomicOr(gp->err, CTR_GATHER_E_RELEASE_TIMEOUT);
+        if (live) gather_store_row(gp, e, grow);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (o.gather_wait_prev && blockIdx.x == 0 && threadIdx.x < 64)
+            gather_wait_prev_lane(gp, o.gather_seq - 1u);
     }
 }
 
@@ -1158,7 +1240,9 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         // reset r from the ring) and r + 2P (the miss sweep took r + P when the ring ran dry):
         // the two map to one slot, and writing both would race (fields of two resets mixed)
         const uint32_t lead = (queued || carried) ? r - (uint32_t)b.epoch[e] - 1u : 0u;   // resets before r
-        const bool fresh = queued && b.pool_r[ps] != r && lead < (uint32_t)b.pool_depth;
+        // (queued or carried alike: a suspended reset the env has passed meanwhile -- a miss sweep
+        // took it -- or whose slot already holds it is dropped, not finished into a stale slot)
+        const bool fresh = (queued || carried) && b.pool_r[ps] != r && lead < (uint32_t)b.pool_depth;
         const uint64_t genv = (uint64_t)(b.env_base + e);
         // every queued entry draws (draws are a pure function of (seed, env, r); one that is not
         // fresh discards its joints), so the pool_r / epoch loads behind `fresh` overlap the
@@ -1185,7 +1269,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             #pragma unroll
             for (int k = 0; k < 3; ++k) tip[k] = rin->tip[odd][k];
             fst = rin->fstat[odd];
-        } else if (fresh || carried) {
+        } else if (fresh) {
             // a reset at least refill_lead resets ahead of its env runs on the budget (again, if it
             // was suspended before); a nearer one finishes here, before the env can need it
             const int budget = (s_budget > 0 && lead >= (uint32_t)b.refill_lead) ? s_budget : 0x7fffffff;
@@ -1194,7 +1278,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
                                   carried ? &rin->fk[odd] : nullptr, &sv, budget);
             fst = st.status;
         }
-        const bool active = fresh || carried;
+        const bool active = fresh;
         const bool ofin = __shfl_xor((int)fin, 1) != 0;
         double otip[3];
         float oq[6];
@@ -1263,9 +1347,16 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 
 // Requeue: every env's resets epoch + 1 .. epoch + P that its pool slots do not hold (after a seed
 // change or a restore).  One atomic per wave: each lane counts its missing resets (a bit mask over
-// j), an exclusive prefix sum over the wave places them.
+// j), an exclusive prefix sum over the wave places them.  The refill's suspended resets are among
+// them (not in the pool), so both carry lists are emptied (wave 0 of workgroup 0).
 __global__ __launch_bounds__(BLOCK) void k_pool_requeue(ctr_batch_t b)
 {
+    if (blockIdx.x == 0 && threadIdx.x < CARRY_SUBS && b.carry) {
+        CarryHdr *ch = static_cast<CarryHdr *>(b.carry);
+        ch->count[0][threadIdx.x] = 0;
+        ch->count[1][threadIdx.x] = 0;
+        if (threadIdx.x == 0) ch->parity = 0;
+    }
     const int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool in = e < b.n;
     const uint32_t r = in ? b.epoch[e] : 0u;

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 12
+CTR_ABI_VERSION = 13
 CTR_IPC_HANDLE_BYTES = 64
 CTR_GATHER_MAX_RANKS = 16
 CTR_MAX_SYSTEMS = 8
@@ -115,13 +115,24 @@ class CtrStepOut(ctypes.Structure):
         ("gather", _P),
         ("gather_prev", _P),
         ("gather_prev_seq", ctypes.c_uint32),
-        ("gather_pad", ctypes.c_uint32),
+        ("gather_seq", ctypes.c_uint32),
+        ("gather_wait_prev", ctypes.c_int32),
+        ("gather_pad", ctypes.c_int32),
     ]
 
 
 class CtrGatherPush(ctypes.Structure):
     _fields_ = [("src", _P), ("n", ctypes.c_int64), ("world", ctypes.c_int32), ("pad", ctypes.c_int32),
-                ("dst", _P * CTR_GATHER_MAX_RANKS), ("seqw", _P * CTR_GATHER_MAX_RANKS), ("ticket", _P)]
+                ("dst", _P * CTR_GATHER_MAX_RANKS), ("seqw", _P * CTR_GATHER_MAX_RANKS), ("ticket", _P),
+                # fused push flow control (ABI 13)
+                ("relw", _P * CTR_GATHER_MAX_RANKS), ("rel", _P), ("wait_seqw", _P), ("err", _P),
+                ("depth", ctypes.c_int32), ("spin_limit", ctypes.c_uint32)]
+
+
+CTR_GATHER_E_WAIT_TIMEOUT = 1       # a consumer wait gave up
+CTR_GATHER_E_OVERWRITTEN = 2        # a sequence word was already past the awaited step
+CTR_GATHER_E_RELEASE_TIMEOUT = 4    # a fused push stored into a slot not yet released
+CTR_GATHER_E_PREV_TIMEOUT = 8       # the fused consumer wait gave up
 
 
 class CtrCopy(ctypes.Structure):

@@ -95,22 +95,31 @@ def max_over_ranks(value, device=None, group=None):
 # (IPC handles exchanged over the process group), and each step's rows go into slot `seq % depth`
 # of every ring, followed by the step's sequence word.  Engines:
 #   "fused"  k_step itself stores each env's row into every rank's slot (ctr_step_out_t.gather:
-#            8 extra 16-B stores per lane at the end of the step), and the NEXT k_step launch
-#            publishes the sequence words (its predecessor has completed, so the rows are
-#            performed); a consumer that waits before the next step publishes them itself
-#            (ctr_gather_publish).  No extra launch, no cross-stream dependency per step.
+#            8 extra 16-B stores per lane at the end of the step, then a system-scope release
+#            fence per wave), and the NEXT k_step launch publishes the sequence words (its
+#            predecessor has completed, so the rows are performed at system scope); a consumer
+#            that waits before the next step publishes them itself (ctr_gather_publish).  No
+#            extra launch, no cross-stream dependency per step.
 #   "sdma"   ctr_copy_list after the step: copy-engine copies (no CU at all) of the packed rows;
 #            measured host-synchronous per copy in this runtime (~25 us each), so it cannot keep
 #            up with a step; kept selectable
 # (A standalone push kernel on a side stream, ctr_gather_push, overlaps the step but each step
 # then waits on a cross-stream event: ~10 us per hop, measured)
-# Layout of a receive ring: [depth][world][n][4] float32, so a slot is the rank-major =
-# global-id-ordered [world * n, 4] gather; sequence words [depth][world] uint32 (word [slot][r] =
-# the last step rank r published into that slot).  Ring and words are uncached device memory:
-# other GPUs write them, so this GPU's L2 must not serve stale lines.
+# Layout of a rank's shared memory: the receive ring [depth][world][n][4] float32 (a slot is the
+# rank-major = global-id-ordered [world * n, 4] gather), and a control block of sequence words
+# [depth][world] uint32 (word [slot][r] = the last step rank r published into that slot), release
+# words [world] uint32 (word [c] = the last step whose slot consumer c released, written by c) and
+# the push kernel's ticket.  Both are uncached device memory: other GPUs write them, so this
+# GPU's L2 must not serve stale lines.
 #
-# Reuse rule: slot s is rewritten by step seq + depth, so a consumer reads step seq before any
-# rank pushes step seq + depth (ctr_gather_wait flags a slot overwritten before it was consumed).
+# Reuse rule (flow control, fused engine): slot s % depth is rewritten by step s + depth.  A rank
+# releases its slot of step s when it launches step s + depth - 1 (the launch's first lanes write
+# the release words of every producer), so a gathered view of step s is valid until this rank
+# launches step s + depth - 1; k_step(t) stores its rows only once every rank has released step
+# t - depth.  With wait_prev (depth >= 3) k_step(t) also waits until every rank's rows of step
+# t - 1 are in this rank's ring, so that slot is readable after the launch (the consumer wait
+# fused into the step).  The sdma engine and ctr_gather_push leave the pacing to the caller
+# (ctr_gather_wait flags a slot overwritten before it was consumed).
 
 class HipCopyOps(object):
     """The device side of PushGather: libctr_reach_amd.so's IPC, uncached memory, descriptor,
@@ -157,19 +166,24 @@ class HipCopyOps(object):
         ev.record(torch.cuda.current_stream(self.device))      # created now, not lazily
         return ev
 
-    def upload_descriptors(self, targets, n, ticket_ptr):
+    def upload_descriptors(self, targets, n, ticket_ptr, flow):
         """Per-slot ctr_gather_push_t descriptors in device memory (the fused push reads them):
-        targets[slot] = [(row block dst, sequence word), ...] per rank.  Returns (keep-alive,
-        device pointer per slot)."""
+        targets[slot] = [(row block dst, sequence word), ...] per rank; flow = the flow-control
+        fields (relw: this rank's release word in every rank, rel, wait_seqw per slot, err, depth,
+        spin_limit).  Returns (keep-alive, device pointer per slot)."""
         import ctypes
         import torch
         size = ctypes.sizeof(self._abi.CtrGatherPush)
         raw = bytearray()
-        for tg in targets:
+        for slot, tg in enumerate(targets):
             g = self._abi.CtrGatherPush()
             g.n, g.world, g.ticket = n, len(tg), ticket_ptr
             for k, (dst, sw) in enumerate(tg):
                 g.dst[k], g.seqw[k] = dst, sw
+            for k, rw in enumerate(flow["relw"]):
+                g.relw[k] = rw
+            g.rel, g.wait_seqw, g.err = flow["rel"], flow["wait_seqw"][slot], flow["err"]
+            g.depth, g.spin_limit = flow["depth"], flow["spin_limit"]
             raw += bytes(g)
         dev = torch.frombuffer(raw, dtype=torch.uint8).to(self.device)
         return dev, [dev.data_ptr() + i * size for i in range(len(targets))]
@@ -236,6 +250,7 @@ class PushGather(object):
       step_args(seq)           (descriptor of seq's slot, descriptor to publish, its seq) for
                                ctr_step_out_t.gather / gather_prev / gather_prev_seq
       stepped(seq)             the step launch with seq was enqueued (its words are pending)
+      wait_prev                ctr_step_out_t.gather_wait_prev for every step (depth >= 3)
     sdma engine:
       push(packed, seq, ready_event, parity)   copy-engine copies of packed ([n + 1, 4]: row n is
                                the sequence row k_step writes with ctr_step_out_t.packed_seq)
@@ -243,10 +258,11 @@ class PushGather(object):
     both:
       wait(seq, stream)        enqueue the consumer wait for step seq (publishing it first if no
                                later step did) and return the gathered [world * n, 4] rows
+    Step numbers are Python ints from 1 (slot = seq % depth); the device sees them modulo 2^32.
     ``ops`` is the device backend (HipCopyOps; tests pass a CPU stand-in)."""
 
-    def __init__(self, n, group=None, depth=2, engine="fused", n_streams=None, device=None, ops=None,
-                 spin_limit=1 << 24):
+    def __init__(self, n, group=None, depth=3, engine="fused", n_streams=None, device=None, ops=None,
+                 spin_limit=1 << 22, wait_prev=False):
         import torch
         import torch.distributed as dist
         if engine not in ("fused", "sdma"):
@@ -254,20 +270,25 @@ class PushGather(object):
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.n, self.depth, self.engine = int(n), int(depth), engine
-        if self.depth < 1:
-            raise ValueError("depth must be >= 1")
+        if self.depth < 2:
+            raise ValueError("depth must be >= 2 (a slot is rewritten depth steps later)")
+        if wait_prev and self.depth < 3:
+            raise ValueError("wait_prev needs depth >= 3 (the view of step t - 1 is read after step t)")
         if self.world > 16:
             raise ValueError("at most 16 ranks (CTR_GATHER_MAX_RANKS)")
+        self.wait_prev = bool(wait_prev)
         self.ops = ops if ops is not None else HipCopyOps(device)
         self.spin_limit = int(spin_limit)
         W, n4 = self.world, self.n * PACK_WIDTH * 4
         self.block_bytes = n4
+        self.rel_off = self.depth * W * 4                 # release words, then the push ticket
+        ticket_off = self.rel_off + W * 4
         # every rank takes part in both exchanges even after a local failure, and all raise
         # together: a rank that gave up alone would leave the others blocked in a collective
         mine, err = None, None
         try:
             self.recv_ptr = self.ops.alloc_shared(self.depth * W * n4)
-            self.seqw_ptr = self.ops.alloc_shared(self.depth * W * 4 + 64)     # + this rank's push ticket
+            self.seqw_ptr = self.ops.alloc_shared(ticket_off + 64)
             mine = (self.ops.handle(self.recv_ptr), self.ops.handle(self.seqw_ptr))
         except Exception as ex:            # noqa: BLE001 -- re-raised below, on every rank
             err = "rank %d: %s" % (self.rank, ex)
@@ -276,7 +297,7 @@ class PushGather(object):
         errs = [e for _, e in allh if e]
         if errs:
             raise RuntimeError("PushGather setup failed: " + "; ".join(errs))
-        self.ticket_ptr = self.seqw_ptr + self.depth * W * 4
+        self.ticket_ptr = self.seqw_ptr + ticket_off
         self.peer_recv, self.peer_seqw = [None] * W, [None] * W
         try:
             for p in range(W):
@@ -291,11 +312,16 @@ class PushGather(object):
             raise RuntimeError("PushGather peer mapping failed: " + "; ".join(errs))
         self.recv = self.ops.view(self.recv_ptr, (self.depth, W, self.n, PACK_WIDTH), torch.float32)
         self.seqw = self.ops.view(self.seqw_ptr, (self.depth, W), torch.int32)
+        self.rel = self.ops.view(self.seqw_ptr + self.rel_off, (W,), torch.int32)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.pending = 0          # fused: the last pushed step whose words are not yet published
         if engine == "fused":
+            flow = {"relw": [self.peer_seqw[p] + self.rel_off + 4 * self.rank for p in range(W)],
+                    "rel": self.seqw_ptr + self.rel_off,
+                    "wait_seqw": [self.seqw_ptr + ((s - 1) % self.depth) * W * 4 for s in range(self.depth)],
+                    "err": self.err.data_ptr(), "depth": self.depth, "spin_limit": self.spin_limit}
             self._desc_keep, self.desc = self.ops.upload_descriptors(
-                [self.targets(s) for s in range(self.depth)], self.n, self.ticket_ptr)
+                [self.targets(s) for s in range(self.depth)], self.n, self.ticket_ptr, flow)
             self.n_streams = 0
         else:
             # the copies to peer (rank + 1 + i) % world go on stream i % n_streams (different engines)
@@ -355,7 +381,19 @@ class PushGather(object):
             self.ops.publish(self.desc[slot], seq, stream)     # no later step has published it
             self.pending = 0
         self.ops.wait(self.seqw_ptr + slot * self.world * 4, self.world, seq, self.spin_limit, self.err, stream)
-        return self.recv[slot].reshape(self.world * self.n, PACK_WIDTH)
+        return self.slot_view(seq)
+
+    def flush(self, stream):
+        """Publish the last pushed step's sequence words now (fused engine: a step's words are
+        otherwise published by the next step's launch) -- for a rank that stops stepping while
+        others still wait for its last step."""
+        if self.engine == "fused" and self.pending:
+            self.ops.publish(self.desc[self.pending % self.depth], self.pending, stream)
+            self.pending = 0
+
+    def slot_view(self, seq):
+        """The gathered [world * n, 4] rows of step seq's slot (valid once its wait has run)."""
+        return self.recv[seq % self.depth].reshape(self.world * self.n, PACK_WIDTH)
 
     def close(self):
         for p in range(self.world):
@@ -364,3 +402,45 @@ class PushGather(object):
                 self.ops.close(self.peer_seqw[p])
         self.ops.free_shared(self.recv_ptr)
         self.ops.free_shared(self.seqw_ptr)
+
+
+def verify_gathered(out, mine, err, group=None):
+    """Bit-compare a gathered slot `out` ([world * n, 4]) with a process-group all_gather of every
+    rank's own rows `mine` ([n, 4]) -- the reference copy -- and agree on the verdict over every
+    rank (MAX all_reduce).  Returns (ok on every rank, report).  Used by bench.py's untimed check of
+    the push gather before any window runs with it."""
+    import torch
+    import torch.distributed as dist
+    ws = dist.get_world_size(group)
+    gloo = dist.get_backend(group) == "gloo"
+    src = mine.cpu() if gloo else mine
+    blocks = [torch.empty_like(src) for _ in range(ws)]
+    dist.all_gather(blocks, src, group=group)
+    ref = torch.cat(blocks)
+    got = out.cpu() if gloo else out
+    bad_rows = int((got != ref).any(dim=1).sum().item())
+    e = int(err.item()) if hasattr(err, "item") else int(err)
+    flags = torch.tensor([1 if bad_rows else 0, e, bad_rows], dtype=torch.int64,
+                         device="cpu" if gloo else out.device)
+    dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+    ok = int(flags[0]) == 0 and int(flags[1]) == 0
+    return ok, {"rows_equal_all_ranks": int(flags[0]) == 0, "err_bits_max": int(flags[1]),
+                "mismatched_rows_max": int(flags[2])}
+
+
+def check_push_steps(step, gather, mine, steps, stream=None, group=None):
+    """bench.py's check of the fused push before any timing: `steps` times, run step(i) (one env
+    step that pushes), wait for its slot and verify_gathered it against the process-group copy of
+    mine() (this rank's own rows of that step).  Stops at the first failure.  Returns the report
+    (``passed``, ``steps_checked``, and on a failure ``failed_at_step`` with verify_gathered's
+    fields); every rank gets the same verdict."""
+    rep = {"steps_checked": 0}
+    for i in range(steps):
+        seq = step(i)
+        ok, r = verify_gathered(gather.wait(seq, stream), mine(), gather.err, group=group)
+        rep["steps_checked"] += 1
+        if not ok:
+            rep.update(r, failed_at_step=i)
+            break
+    rep["passed"] = "failed_at_step" not in rep
+    return rep

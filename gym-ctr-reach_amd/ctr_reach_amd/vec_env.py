@@ -282,8 +282,7 @@ class CtrReachVecEnv(object):
         """Drop the refill queue and queue every env's next pool_depth resets the pool does not
         hold (ctr_pool_requeue), then refill: after a seed change or a checkpoint restore."""
         self.refill[0] = 0
-        if self.carry is not None:
-            self.carry.zero_()           # suspended resets: the requeue below queues them again
+        # (the requeue also empties the refill's suspended lists: it queues their resets again)
         rc = self.lib.ctr_pool_requeue(self.cfg, self._batch, _abi.stream_ptr(stream))
         _abi.check(rc, "ctr_pool_requeue")
         self._steps_since_refill = 0
@@ -382,10 +381,11 @@ class CtrReachVecEnv(object):
         g = self._push_gather
         fused = g is not None and g.engine == "fused"
         if fused:                              # this step also stores its rows into every rank's ring
-            self.gather_seq = self.gather_seq + 1 if self.gather_seq < 0xFFFFFFFF else 1
+            self.gather_seq += 1               # a Python int (slot = seq % depth); modulo 2^32 on the device
             cur, prev, prev_seq = g.step_args(self.gather_seq)
             o = self._out
-            o.gather, o.gather_prev, o.gather_prev_seq = cur, prev, prev_seq
+            o.gather, o.gather_prev, o.gather_prev_seq = cur, prev, prev_seq & 0xFFFFFFFF
+            o.gather_seq, o.gather_wait_prev = self.gather_seq & 0xFFFFFFFF, 1 if g.wait_prev else 0
         mode = _abi.AUTORESET_OFF
         if self.autoreset:
             # no done env can miss its pooled reset while at most pool_depth steps have run since
@@ -403,6 +403,7 @@ class CtrReachVecEnv(object):
             rc = self.lib.ctr_step(self.cfg, self._batch, _abi.ptr(actions), self._out, mode, sp)
         if fused:
             o.gather = o.gather_prev = None    # only this launch pushes (other ctr_step users of _out do not)
+            o.gather_wait_prev = 0
             if rc == 0:
                 g.stepped(self.gather_seq)
         if rc:
@@ -525,11 +526,14 @@ class CtrReachVecEnv(object):
         out["table"] = table
         return out
 
-    def enable_gather(self, backend="push", group=None, depth=2):
+    def enable_gather(self, backend="push", group=None, depth=3, wait_prev=False):
         """Set up the push all-gather (collective: every rank calls it).  "push": every later
         step also stores its packed rows into every rank's receive ring (the fused push; no
-        extra launch); "sdma": gather_outputs(backend="sdma") copies them with the copy engines
-        (needs pack_outputs=True).  Returns the distributed.PushGather."""
+        extra launch), paced by the ranks' slot releases: the gathered view of step s stays valid
+        until this env launches step s + depth - 1; with ``wait_prev`` every step also waits until
+        the previous step's rows of every rank are in this rank's ring (depth >= 3).  "sdma":
+        gather_outputs(backend="sdma") copies them with the copy engines (needs
+        pack_outputs=True; the caller paces the ranks).  Returns the distributed.PushGather."""
         if self._push_gather is not None:
             raise RuntimeError("the gather is already enabled")
         if backend == "sdma" and self.packed_bufs is None:
@@ -537,10 +541,11 @@ class CtrReachVecEnv(object):
         if backend not in ("push", "sdma"):
             raise ValueError("backend must be 'push' or 'sdma'")
         self._push_gather = D.PushGather(self.num_envs, group=group, depth=depth, device=self.device,
-                                         engine="fused" if backend == "push" else "sdma")
+                                         engine="fused" if backend == "push" else "sdma",
+                                         wait_prev=wait_prev and backend == "push")
         return self._push_gather
 
-    def gather_outputs(self, group=None, async_op=False, backend="rccl", depth=2):
+    def gather_outputs(self, group=None, async_op=False, backend="rccl", depth=3):
         """Optional collective for a single-process trainer: every rank's last-step (tip, reward,
         done, success) packed to 16 B/env and all-gathered -> [world * n, 4] float32 in global-id
         order.  Not used on the stepping path.  async_op=True returns (out, work) and lets the
@@ -552,7 +557,9 @@ class CtrReachVecEnv(object):
         "sdma" (copy engines, needs pack_outputs=True; set up on first use, collectively): this
         rank's rows land in every rank's IPC-mapped receive ring (distributed.PushGather); ``out``
         is slot (step % depth) of this rank's ring, valid after ``work.wait()`` (which enqueues
-        the wait for every rank's block on the current stream) until step + depth is gathered.
+        the wait for every rank's block on the current stream) until this env launches step +
+        depth - 1 (push: the step kernels pace the ranks by their slot releases; sdma: the caller
+        paces them).
 
         With ``pack_outputs=True`` the step kernel itself wrote the packed rows (no packing
         launch); otherwise they are packed here from the step's outputs."""

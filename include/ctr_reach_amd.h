@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 12
+#define CTR_ABI_VERSION 13
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -202,17 +202,30 @@ typedef struct ctr_step_out_t {
                                     that ctr_copy_list pushes after the rows (packed then holds
                                     n + 1 rows).  0: row n is not touched.                        */
     uint32_t  packed_pad;
-    const ctr_gather_push_t *gather;      /* device or NULL: the fused push gather -- k_step also
+    const ctr_gather_push_t *gather;      /* device or NULL: the fused push gather of step
+                                             gather_seq (descriptor of its slot) -- k_step also
                                              stores each env's packed row (as in `packed`) into
                                              every rank's receive slot, gather->dst[p] + e for
-                                             p < gather->world (IPC-mapped peer memory)          */
+                                             p < gather->world (IPC-mapped peer memory), after
+                                             every rank has released that slot (flow control,
+                                             see "Push all-gather"); every storing wave then
+                                             ends with a system-scope release fence.  The first
+                                             lanes also release this rank's slot of step
+                                             gather_seq + 1 - depth to every producer          */
     const ctr_gather_push_t *gather_prev; /* device or NULL: the first lanes of k_step publish
                                              gather_prev_seq to every gather_prev->seqw[p]
                                              (release, system scope) -- the previous gathered
                                              step, whose launch has completed (so its row stores
-                                             are performed) before this one starts               */
+                                             are performed at system scope) before this one
+                                             starts                                              */
     uint32_t  gather_prev_seq;
-    uint32_t  gather_pad;
+    uint32_t  gather_seq;        /* the step pushed with `gather` (wraps modulo 2^32)            */
+    int32_t   gather_wait_prev;  /* != 0 (with gather, depth >= 3): k_step also waits until every
+                                    rank's rows of step gather_seq - 1 are published in this
+                                    rank's ring (gather->wait_seqw), so after this launch the
+                                    previous step's gathered slot is readable on the stream (the
+                                    fused consumer wait; errors in gather->err)                  */
+    int32_t   gather_pad;
 } ctr_step_out_t;
 
 /* ---------------------------------------------------------------------------------------
@@ -373,7 +386,10 @@ int64_t ctr_refill_carry_bytes(int64_t carry_cap);
 
 /* Queue every environment's next pool_depth resets (epoch + 1 .. epoch + P) that its pool slots
  * do not hold, e.g. after the batch state was restored from a checkpoint or the seed changed;
- * the next ctr_pool_refill computes them. */
+ * the next ctr_pool_refill computes them.  Also empties both of the refill's suspended lists
+ * (batch->carry: their resets are not in the pool, so they are queued again).  A suspended reset
+ * the refill finds its environment has passed (a miss sweep computed it) or its slot already
+ * holding is dropped, as a queued one is. */
 int ctr_pool_requeue(const ctr_env_config_t *cfg, const ctr_batch_t *batch, void *stream);
 
 /* The tube table each environment's current episode uses (Model.current_sys_parameters,
@@ -397,13 +413,31 @@ int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr
  * A consumer waits for a step with ctr_gather_wait.  The host side
  * (ctr_reach_amd.distributed.PushGather) plans the destinations: receive ring
  * [depth][world][n][4] float32 (rank-major = global env id order within a slot), sequence words
- * [depth][world] uint32.
+ * [depth][world] uint32, release words [world] uint32.
+ *
+ * Ordering of the fused push (ABI 13).  Step t's rows are stored by the waves of k_step(t); each
+ * storing wave ends with a system-scope release fence (its stores are performed at system scope
+ * before the wave ends), and k_step(t + 1), which the stream starts only after k_step(t) has
+ * completed, publishes t's sequence words with system-scope release stores.  A consumer that
+ * acquires the words (system scope) therefore reads rows at least as new as step t.
+ * Flow control: slot t % depth is rewritten by step t + depth.  Consumer c releases its slot of
+ * step s when it launches step s + depth - 1 (k_step's first lanes store s into every producer's
+ * release word for c), so a gathered view of step s stays valid until this rank launches step
+ * s + depth - 1; a producer's k_step(t) stores its rows only after every consumer has released
+ * step t - depth (a bounded wait; on time-out the rows are stored anyway and err gets
+ * CTR_GATHER_E_RELEASE_TIMEOUT).  ctr_gather_push and ctr_copy_list do not take part in the
+ * flow control: their callers pace the ranks.
  * ------------------------------------------------------------------------------------- */
 #define CTR_IPC_HANDLE_BYTES 64
 #define CTR_GATHER_MAX_RANKS 16
+/* err bits of ctr_gather_wait and of the fused push (ctr_gather_push_t.err) */
+#define CTR_GATHER_E_WAIT_TIMEOUT    1u   /* a consumer wait gave up after spin_limit polls      */
+#define CTR_GATHER_E_OVERWRITTEN     2u   /* a sequence word was already past the awaited step   */
+#define CTR_GATHER_E_RELEASE_TIMEOUT 4u   /* a fused push stored into a slot not yet released    */
+#define CTR_GATHER_E_PREV_TIMEOUT    8u   /* the fused consumer wait (gather_wait_prev) gave up  */
 
 /* One rank's push of its block: the host struct of ctr_gather_push, and (in device memory) the
- * per-slot descriptor of the fused push (ctr_step_out_t.gather; src, n and ticket unused there). */
+ * per-slot descriptor of the fused push (ctr_step_out_t.gather; src and ticket unused there). */
 struct ctr_gather_push_t {
     const void *src;                          /* [n][4] float32 packed rows (16-B aligned)     */
     int64_t     n;
@@ -414,11 +448,20 @@ struct ctr_gather_push_t {
     uint32_t   *seqw[CTR_GATHER_MAX_RANKS];   /* this block's sequence word in rank p's memory  */
     uint32_t   *ticket;                       /* this rank's device word, zero-initialised (the
                                                  kernel leaves it zero)                      */
+    /* fused push only (ABI 13): */
+    uint32_t   *relw[CTR_GATHER_MAX_RANKS];   /* this rank's release word in rank p's memory   */
+    const uint32_t *rel;                      /* [world] this rank's release words: rel[c] = the
+                                                 last step whose slot consumer c released   */
+    const uint32_t *wait_seqw;                /* [world] this rank's sequence words of the
+                                                 previous slot (gather_wait_prev)           */
+    uint32_t   *err;                          /* device word: CTR_GATHER_E_* bits             */
+    int32_t     depth;                        /* ring slots (>= 2)                            */
+    uint32_t    spin_limit;                   /* polls before a wait gives up (~0.2 us each)  */
 };
 
 /* Enqueue the push kernel: the n rows to every dst[p] (p < world), then seq to every seqw[p]
  * (after all rows, release at system scope).  workgroups: grid size (e.g. 128); its waves use
- * ~20 VGPRs and no LDS, so they share SIMDs with k_step waves. */
+ * ~20 VGPRs and no LDS, so they share SIMDs with k_step waves.  No flow control (see above). */
 int ctr_gather_push(const ctr_gather_push_t *g, uint32_t seq, int32_t workgroups, void *stream);
 
 /* Publish seq to every g_dev->seqw[p] (release, system scope) after the work already on

@@ -189,19 +189,52 @@ class _ShmCopyOps(object):
     def native_plan(self, copies):
         return None
 
-    def upload_descriptors(self, targets, n, ticket_ptr):
-        return None, [list(t) for t in targets]
+    def upload_descriptors(self, targets, n, ticket_ptr, flow):
+        return None, [dict(flow, targets=list(t), wait_seqw=flow["wait_seqw"][s]) for s, t in enumerate(targets)]
 
     def publish(self, desc, seq, stream):
         import ctypes
-        for dst, sw in desc:
-            ctypes.c_uint32.from_address(sw).value = seq
+        for dst, sw in desc["targets"]:
+            ctypes.c_uint32.from_address(sw).value = seq & 0xFFFFFFFF
 
-    def fused_step_stores(self, desc, rows):
-        """What k_step does with ctr_step_out_t.gather: every env's row into every target."""
+    def fused_step(self, cur, prev, prev_seq, seq, rows, wait_prev=False):
+        """What k_step does with ctr_step_out_t.gather (csrc/ctr_kernels.hip step_body), in its
+        order: publish the previous step's words, release this rank's slot of step seq + 1 -
+        depth, wait (bounded) until every rank released step seq - depth, store every env's row
+        into every target, then (gather_wait_prev) wait for every rank's words of step seq - 1."""
         import ctypes
-        for dst, sw in desc:
+        import time
+        u32 = ctypes.c_uint32
+        err = u32.from_address(cur["err"])
+        if prev is not None:
+            self.publish(prev, prev_seq, None)
+        for rw in cur["relw"]:
+            u32.from_address(rw).value = (seq + 1 - cur["depth"]) & 0xFFFFFFFF
+        W = len(cur["targets"])
+        rel = (u32 * W).from_address(cur["rel"])
+
+        def reached(a, b):
+            return ((a - b) & 0xFFFFFFFF) < 0x80000000
+
+        for k in range(cur["spin_limit"] + 1):
+            if all(reached(r, (seq - cur["depth"]) & 0xFFFFFFFF) for r in rel):
+                break
+            time.sleep(0.0005)
+        else:
+            err.value |= 4                                   # CTR_GATHER_E_RELEASE_TIMEOUT
+        for dst, sw in cur["targets"]:
             ctypes.memmove(dst, rows.data_ptr(), rows.numel() * 4)
+        if wait_prev:
+            words = (u32 * W).from_address(cur["wait_seqw"])
+            want = (seq - 1) & 0xFFFFFFFF
+            for k in range(cur["spin_limit"] + 1):
+                if all(reached(w, want) for w in words):
+                    if any(w != want for w in words):
+                        err.value |= 2                       # CTR_GATHER_E_OVERWRITTEN
+                    break
+                time.sleep(0.0005)
+            else:
+                err.value |= 8                               # CTR_GATHER_E_PREV_TIMEOUT
 
     def copy_list(self, plan, streams, ready_event, done_events):
         import ctypes
@@ -245,9 +278,7 @@ def _ce_worker(rank, world, port, n, engine, q):
                 g.push(packed, seq, None)
             else:                      # the env's fused step: rows now, words by the next step
                 cur, prev, prev_seq = g.step_args(seq)
-                if prev is not None:
-                    ops.publish(prev, prev_seq, None)
-                ops.fused_step_stores(cur, packed[:n])
+                ops.fused_step(cur, prev, prev_seq, seq, packed[:n])
                 g.stepped(seq)
         got = []
         for seq in range(1, 6):
@@ -268,6 +299,9 @@ def _ce_worker(rank, world, port, n, engine, q):
         dist.barrier()
         g.wait(3, None)
         overrun = int(g.err[0])
+        if engine == "fused":
+            # the release words: rank c released step 6 + 1 - depth = 4 in every producer
+            np.testing.assert_array_equal(g.rel.numpy(), [4] * world)
         if rank == 0:
             q.put((torch.stack(got).numpy(), g.seqw.numpy().copy(), overrun))
         dist.barrier()
@@ -342,3 +376,136 @@ def test_push_gather_setup_failure_raises_on_every_rank():
         assert p.exitcode == 0
     for r in range(world):
         assert "peer mapping failed" in got[r] and "rank 1" in got[r], got
+
+
+def _rows(n, rank, seq):
+    """A rank's packed block of step seq in the stand-in tests (distinct per rank and step)."""
+    return (torch.arange(n * 4, dtype=torch.float32).reshape(n, 4) + 1000 * rank + 1e5 * seq).contiguous()
+
+
+def _flow_worker(rank, world, port, n, steps, mode, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = None
+    try:
+        import time
+        from ctr_reach_amd import distributed as D
+        ops = _ShmCopyOps()
+        wait_prev = mode == "wait_prev"
+        g = D.PushGather(n, depth=3, engine="fused", ops=ops, spin_limit=20000, wait_prev=wait_prev)
+        rng = np.random.default_rng(rank)
+        views = []
+        for seq in range(1, steps + 1):
+            if wait_prev:
+                # ranks run free (no barrier): rank 0 fast, the last rank slow, the others jittered
+                time.sleep(0.0 if rank == 0 else (0.02 if rank == world - 1 else float(rng.uniform(0, 0.01))))
+            cur, prev, prev_seq = g.step_args(seq)
+            ops.fused_step(cur, prev, prev_seq, seq, _rows(n, rank, seq), wait_prev=wait_prev)
+            g.stepped(seq)
+            if wait_prev and seq >= 2:
+                # after step seq (its fused wait), the view of step seq - 1 is complete and stays
+                # valid until this rank launches step seq + 1: read it now, slowly
+                time.sleep(0.003)
+                views.append((seq - 1, g.slot_view(seq - 1).clone()))
+            elif mode == "rank0_consumes" and rank == 0:
+                # only rank 0 consumes, slowly, through the explicit wait; the producers run
+                # without any wait and are held back only by rank 0's slot releases
+                g.wait(seq, None)
+                time.sleep(0.02)
+                views.append((seq, g.slot_view(seq).clone()))
+        g.flush(None)                      # the last step's words (no next launch publishes them)
+        q.put((rank, [(s, v.numpy()) for s, v in views], int(g.err[0])))
+        dist.barrier()
+    finally:
+        if g is not None:
+            g.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["wait_prev", "rank0_consumes"])
+def test_push_gather_flow_control_free_running_ranks(mode):
+    """The fused push's flow control (slot releases + the fused consumer wait, as k_step runs
+    them, emulated on the CPU stand-in) with ranks that run free at different speeds -- every rank
+    consuming through the fused wait, or only rank 0 consuming (slowly) while the others push with
+    no wait at all: every view a rank reads holds exactly every rank's rows of its step, and no
+    wait times out."""
+    world, n, steps = 3, 8, 14
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_flow_worker, args=(r, world, port, n, steps, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, views, err in got:
+        assert err == 0, (rank, err)
+        if mode == "wait_prev":
+            assert [s for s, _ in views] == list(range(1, steps))
+        else:
+            assert [s for s, _ in views] == (list(range(1, steps + 1)) if rank == 0 else [])
+        for s, v in views:
+            want = np.concatenate([_rows(n, r, s).numpy() for r in range(world)])
+            np.testing.assert_array_equal(v, want, err_msg="rank %d, step %d" % (rank, s))
+
+
+def _check_worker(rank, world, port, n, corrupt_at, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = None
+    try:
+        import ctypes
+        from ctr_reach_amd import distributed as D
+        ops = _ShmCopyOps()
+        g = D.PushGather(n, depth=3, engine="fused", ops=ops, spin_limit=20000)
+        cur_rows = {}
+
+        def step(i):
+            seq = i + 1
+            cur, prev, prev_seq = g.step_args(seq)
+            cur_rows["mine"] = _rows(n, rank, seq)
+            ops.fused_step(cur, prev, prev_seq, seq, cur_rows["mine"])
+            g.stepped(seq)
+            dist.barrier()                 # every rank's rows of seq stored
+            if i == corrupt_at and rank == 1:
+                # one float of rank 0's block in rank 1's ring goes bad (a stale or torn row)
+                ctypes.c_float.from_address(g.recv_ptr + (seq % g.depth) * world * n * 16 + 20).value = -7.0
+            dist.barrier()
+            return seq
+        rep = D.check_push_steps(step, g, lambda: cur_rows["mine"], 5)
+        q.put((rank, rep))
+        dist.barrier()
+    finally:
+        if g is not None:
+            g.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt_at", [None, 2])
+def test_push_check_fails_on_every_rank_for_a_corrupted_slot(corrupt_at):
+    """bench.py's pre-window check of the push gather (distributed.check_push_steps): a clean run
+    passes every step; one corrupted float in ONE rank's ring makes the check fail on EVERY rank
+    at that step (so every rank falls back to RCCL together), with the mismatch counted."""
+    world, n = 2, 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, n, corrupt_at, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        rep = got[r]
+        if corrupt_at is None:
+            assert rep["passed"] and rep["steps_checked"] == 5, rep
+        else:
+            assert not rep["passed"] and rep["failed_at_step"] == corrupt_at, rep
+            assert rep["steps_checked"] == corrupt_at + 1 and rep["mismatched_rows_max"] == 1, rep
+            assert not rep["rows_equal_all_ranks"] and rep["err_bits_max"] == 0, rep

@@ -110,11 +110,13 @@ def _two_rank_worker(rank, world, port, n, backend, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("backend", ["push", "sdma"])
-def test_push_gather_two_processes_one_gpu(cuda, backend):
-    """Two ranks on cuda:0, each mapping the other's receive ring and sequence words (IPC)."""
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("backend,world", [("push", 2), ("push", 8), ("sdma", 2)])
+def test_push_gather_two_processes_one_gpu(cuda, backend, world):
+    """`world` ranks on cuda:0, each mapping every other rank's receive ring, sequence words and
+    release words (IPC): the 8-peer ring layout and handle exchange of configs[3] minus xGMI."""
     import torch.multiprocessing as mp
-    world, n = 2, 2048
+    n = 2048
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -122,7 +124,7 @@ def test_push_gather_two_processes_one_gpu(cuda, backend):
     for p in procs:
         p.start()
     try:
-        errs = q.get(timeout=100)
+        errs = q.get(timeout=240)
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -131,3 +133,69 @@ def test_push_gather_two_processes_one_gpu(cuda, backend):
     assert all(p.exitcode == 0 for p in procs)
     for i, equal, err in errs:
         assert equal and err == 0, (i, equal, err)
+
+
+def _free_worker(rank, world, port, n, steps, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import time
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ctr_reach_amd import CtrReachVecEnv
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        env = CtrReachVecEnv(n, device=dev, seed=5, env_base=rank * n, pack_outputs=True, max_steps_per_episode=3)
+        env.reset()
+        g = env.enable_gather("push", depth=3, wait_prev=True)
+        rng = np.random.default_rng(20 + rank)
+        own, views = [], []
+        for i in range(steps):
+            if rank == world - 1:
+                time.sleep(0.01)               # one slow rank; no barrier anywhere in the loop
+            env.step(_acts(env, rng))
+            own.append(env.packed_outputs().clone())
+            if i >= 1:
+                # k_step(seq)'s fused wait completed every rank's rows of seq - 1 in this ring; the
+                # view stays valid until this rank launches seq + 1 (depth 3): copy it now
+                views.append(g.slot_view(env.gather_seq - 1).clone())
+        g.flush(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        res = []
+        for s in range(steps - 1):
+            blocks = [torch.empty_like(own[s].cpu()) for _ in range(world)]
+            dist.all_gather(blocks, own[s].cpu())
+            res.append(bool(torch.equal(views[s].cpu(), torch.cat(blocks))))
+        if rank == 0:
+            q.put((res, int(g.err.item())))
+        dist.barrier()
+        g.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_push_gather_free_running_ranks_one_gpu(cuda, world):
+    """The fused push as bench.py runs it (depth 3, the fused consumer wait, slot releases) with
+    ranks on cuda:0 that never synchronise in the step loop, one of them slow: after every step
+    the previous step's slot holds every rank's rows bit for bit, and no wait or release times
+    out."""
+    import torch.multiprocessing as mp
+    n, steps = 2048, 10
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_free_worker, args=(r, world, port, n, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res, err = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    assert err == 0 and all(res), (res, err)

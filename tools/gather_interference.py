@@ -20,7 +20,7 @@ Gathers:
 
 Prints us per step with no gather, and with the gather overlapping the next step.  Also the
 host time per ctr_copy_list call and the copies' own duration.
-usage: python tools/gather_interference.py fused [peers]
+usage: python tools/gather_interference.py fused [peers] [wait]
        python tools/gather_interference.py push [peers] [workgroups]
        python tools/gather_interference.py sdma [peers] [streams]
        python tools/gather_interference.py fake [gather_us] [blocks]"""
@@ -53,24 +53,34 @@ torch.cuda.synchronize()
 if mode == "fused":
     from ctr_reach_amd.distributed import HipCopyOps
     peers = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    wait_prev = len(sys.argv) > 3 and sys.argv[3] == "wait"
+    D = 3
     block = n * 16
     ops = HipCopyOps(dev)
-    ring = ops.alloc_shared(2 * peers * block + 4096)
-    seqw = ring + 2 * peers * block
+    ring = ops.alloc_shared(D * peers * block + 4096)
+    seqw = ring + D * peers * block                # [D][peers] words, then [peers] release words
+    relw = seqw + 4 * D * peers
+    gerr = torch.zeros(1, dtype=torch.int32, device=dev)
 
     class LocalFused(object):
-        """PushGather's fused engine with `peers` local destination blocks per slot."""
+        """PushGather's fused engine (depth 3) with `peers` local destination blocks per slot and
+        the flow control's release words local too (this rank releases for every 'peer')."""
         engine = "fused"
+        depth = D
 
         def __init__(self):
+            flow = {"relw": [relw + 4 * i for i in range(peers)], "rel": relw,
+                    "wait_seqw": [seqw + 4 * peers * ((s - 1) % D) for s in range(D)],
+                    "err": gerr.data_ptr(), "depth": D, "spin_limit": 1 << 22}
             self.keep, self.desc = ops.upload_descriptors(
-                [[(ring + (s * peers + i) * block, seqw + 4 * (s * peers + i)) for i in range(peers)] for s in range(2)],
-                n, seqw + 2048)
+                [[(ring + (s * peers + i) * block, seqw + 4 * (s * peers + i)) for i in range(peers)] for s in range(D)],
+                n, seqw + 2048, flow)
             self.pending = 0
+            self.wait_prev = wait_prev
 
         def step_args(self, seq):
             prev = self.pending
-            return self.desc[seq % 2], (self.desc[prev % 2] if prev else None), prev
+            return self.desc[seq % D], (self.desc[prev % D] if prev else None), prev
 
         def stepped(self, seq):
             self.pending = seq
@@ -86,7 +96,7 @@ if mode == "fused":
 
     def wait_before_step(comp):
         pass
-    label = "fused push into %d blocks" % peers
+    label = "fused push into %d blocks%s" % (peers, " + fused wait" if wait_prev else "")
 elif mode == "push":
     peers = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     wg = int(sys.argv[3]) if len(sys.argv) > 3 else 128
@@ -265,4 +275,6 @@ for rep in range(3):
     if host_us:
         hs = sorted(host_us[-200:])
         line += "   host per gather call: median %.1f us" % hs[len(hs) // 2]
+    if mode == "fused":
+        line += "   err %d" % int(gerr.item())
     print(line, flush=True)
