@@ -229,7 +229,13 @@ __device__ __forceinline__ int32_t *miss_counter(const ctr_batch_t &b) { return 
 __device__ __forceinline__ int32_t *miss_items(const ctr_batch_t &b) { return b.work + 2; }
 
 // The fused push gather (ctr_step_out_t.gather): env e's packed row into every rank's receive
-// slot (IPC-mapped peer memory; the descriptor's pointers are wave-uniform scalar loads).
+// slot (IPC-mapped peer memory; the descriptor's pointers are wave-uniform scalar loads) with
+// system-scope stores (sc0 sc1: written through, not held in this GPU's L2), then one wait for
+// all of them (gather_rows_performed): the rows are performed at system scope before the wave
+// ends, with no L2 write-back.  (A system-scope release fence per wave did the same through a
+// write-back of the whole XCD L2: +15 us per step, tools/gather_interference.py.)  The stores are
+// inline asm, invisible to the compiler's wait counting: the caller waits for them right after
+// (vmcnt(0): nothing is in flight afterwards, so the compiler's later waits stay conservative).
 typedef unsigned int row16_t __attribute__((ext_vector_type(4)));   // one packed row
 
 __device__ __forceinline__ void gather_store_row(const ctr_gather_push_t *g, int64_t e, float4 row)
@@ -237,26 +243,37 @@ __device__ __forceinline__ void gather_store_row(const ctr_gather_push_t *g, int
     const row16_t v = {__float_as_uint(row.x), __float_as_uint(row.y), __float_as_uint(row.z),
                        __float_as_uint(row.w)};
     const int W = g->world;
-    for (int k = 0; k < W; ++k) __builtin_nontemporal_store(v, static_cast<row16_t *>(g->dst[k]) + e);
+    for (int k = 0; k < W; ++k) {
+        row16_t *dst = static_cast<row16_t *>(g->dst[k]) + e;
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(dst), "v"(v) : "memory");
+    }
 }
 
-// Lane k < world publishes seq into rank k's sequence word (release, system scope).
+__device__ __forceinline__ void gather_rows_performed()
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Lane k < world publishes seq into rank k's sequence word (a system-scope store).  Called only
+// after the kernel that pushed step seq has completed, whose waves each waited for their rows'
+// system-scope stores: the rows are performed, so a relaxed store orders after them (a release
+// would add a write-back of this XCD's L2 at the start of every step).
 __device__ __forceinline__ void gather_publish_lane(const ctr_gather_push_t *g, uint32_t seq)
 {
     if ((int)threadIdx.x < g->world)
-        __hip_atomic_store(g->seqw[threadIdx.x], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(g->seqw[threadIdx.x], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Sequence numbers wrap modulo 2^32: a has reached b.
 __device__ __forceinline__ bool seq_reached(uint32_t a, uint32_t b) { return (int32_t)(a - b) >= 0; }
 
 // Fused push flow control (include/ctr_reach_amd.h, "Push all-gather"): lane k < world stores
-// `released` into this rank's release word in rank k's memory (release, system scope; the
+// `released` into this rank's release word in rank k's memory (a system-scope store; the
 // launch's stream predecessors, which held this rank's reads of the released slot, are complete).
 __device__ __forceinline__ void gather_release_lane(const ctr_gather_push_t *g, uint32_t released)
 {
     if ((int)threadIdx.x < g->world)
-        __hip_atomic_store(g->relw[threadIdx.x], released, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(g->relw[threadIdx.x], released, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // This lane's release word of consumer (lane) -- ~0u for lanes >= world (always free).
@@ -285,14 +302,15 @@ __device__ __noinline__ bool gather_wait_slot(const ctr_gather_push_t *g, uint32
 }
 
 // The fused consumer wait (ctr_step_out_t.gather_wait_prev): lane k < world polls this rank's
-// sequence word of rank k's block of the previous slot until it reaches seq (acquire, system
-// scope); bounded, errors into g->err.
+// sequence word of rank k's block of the previous slot until it reaches seq (system-scope loads;
+// the slot's readers are later kernels, and the ring is uncached: no stale line to invalidate);
+// bounded, errors into g->err.
 __device__ __noinline__ void gather_wait_prev_lane(const ctr_gather_push_t *g, uint32_t seq)
 {
     const int lane = (int)threadIdx.x;
     if (lane >= g->world) return;
     for (uint32_t k = 0;; ++k) {
-        const uint32_t v = __hip_atomic_load(g->wait_seqw + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t v = __hip_atomic_load(g->wait_seqw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (seq_reached(v, seq)) {
             if (v != seq) atomicOr(g->err, CTR_GATHER_E_OVERWRITTEN);
             return;
@@ -841,14 +859,13 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     }
     if (gp) {
         // the fused push (every lane of the wave here): once every consumer has released the
-        // slot (normally known since the staging), each env's row into every rank's ring, then a
-        // system-scope release, so the rows are performed at system scope before the wave ends
-        // and the next launch publishes the sequence words (include/ctr_reach_amd.h)
+        // slot (normally known since the staging), each env's row into every rank's ring with
+        // system-scope stores, waited on, so the rows are performed at system scope before the
+        // wave ends and the next launch publishes the sequence words (include/ctr_reach_amd.h)
         if (!slot_free0 && !gather_wait_slot(gp, o.gather_seq) && (threadIdx.x & 63) == 0)
             atomicOr(gp->err, CTR_GATHER_E_RELEASE_TIMEOUT);
         if (live) gather_store_row(gp, e, grow);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gather_rows_performed();
         if (o.gather_wait_prev && blockIdx.x == 0 && threadIdx.x < 64)
             gather_wait_prev_lane(gp, o.gather_seq - 1u);
     }

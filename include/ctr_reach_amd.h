@@ -208,13 +208,13 @@ typedef struct ctr_step_out_t {
                                              every rank's receive slot, gather->dst[p] + e for
                                              p < gather->world (IPC-mapped peer memory), after
                                              every rank has released that slot (flow control,
-                                             see "Push all-gather"); every storing wave then
-                                             ends with a system-scope release fence.  The first
+                                             see "Push all-gather"), as system-scope stores the
+                                             storing wave waits for.  The first
                                              lanes also release this rank's slot of step
                                              gather_seq + 1 - depth to every producer          */
     const ctr_gather_push_t *gather_prev; /* device or NULL: the first lanes of k_step publish
                                              gather_prev_seq to every gather_prev->seqw[p]
-                                             (release, system scope) -- the previous gathered
+                                             (system scope) -- the previous gathered
                                              step, whose launch has completed (so its row stores
                                              are performed at system scope) before this one
                                              starts                                              */
@@ -415,11 +415,12 @@ int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr
  * [depth][world][n][4] float32 (rank-major = global env id order within a slot), sequence words
  * [depth][world] uint32, release words [world] uint32.
  *
- * Ordering of the fused push (ABI 13).  Step t's rows are stored by the waves of k_step(t); each
- * storing wave ends with a system-scope release fence (its stores are performed at system scope
- * before the wave ends), and k_step(t + 1), which the stream starts only after k_step(t) has
- * completed, publishes t's sequence words with system-scope release stores.  A consumer that
- * acquires the words (system scope) therefore reads rows at least as new as step t.
+ * Ordering of the fused push (ABI 13).  Step t's rows are stored by the waves of k_step(t) with
+ * system-scope stores (sc0 sc1: written through this GPU's L2) that each storing wave waits for
+ * before it ends (performed at system scope), and k_step(t + 1), which the stream starts only
+ * after k_step(t) has completed, publishes t's sequence words with system-scope stores.  A
+ * consumer that acquires the words (system scope) therefore reads rows at least as new as step
+ * t; the receive ring is uncached device memory, so the consumer's own L2 holds no stale line.
  * Flow control: slot t % depth is rewritten by step t + depth.  Consumer c releases its slot of
  * step s when it launches step s + depth - 1 (k_step's first lanes store s into every producer's
  * release word for c), so a gathered view of step s stays valid until this rank launches step
@@ -464,7 +465,7 @@ struct ctr_gather_push_t {
  * ~20 VGPRs and no LDS, so they share SIMDs with k_step waves.  No flow control (see above). */
 int ctr_gather_push(const ctr_gather_push_t *g, uint32_t seq, int32_t workgroups, void *stream);
 
-/* Publish seq to every g_dev->seqw[p] (release, system scope) after the work already on
+/* Publish seq to every g_dev->seqw[p] (system scope) after the work already on
  * `stream`: the fused push's explicit publication of its last step (k_step publishes the previous
  * step itself, ctr_step_out_t.gather_prev).  g_dev: device descriptor.  One wave. */
 int ctr_gather_publish(const ctr_gather_push_t *g_dev, uint32_t seq, void *stream);

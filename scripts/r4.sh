@@ -4,10 +4,11 @@
 #   bench    headline bench x2 (+ CPU baseline once) and the two-rank gloo rehearsal on one GPU
 #            (exercises the push gather's pre-window check, calibration and post-window check)
 #   interf   fused push into 8 blocks on one GPU: its per-step cost with and without the fused
-#            consumer wait, and with the A/B library without the storing waves' release fence
-#            (gym-ctr-reach_amd/ctr_reach_amd/lib/libab_nofence.so, built here from a patched copy)
+#            consumer wait
+#   profile  scripts/profile.sh r04 (kernel trace + PMC passes; tools/summarize_profile.py r04 here)
 #   traffic  k_step / k_refill FETCH_SIZE and WRITE_SIZE at the bench's --steps 20, with the
 #            default refill budget and with --refill-budget 0
+#   ab       A/B of the default library against the libraries named in $AB (lib/ file names)
 #   fake     RCCL-footprint stand-in at 2-32 workgroups (channel caps), durations from a per-channel
 #            bandwidth model; needs tools/libfake_gather.so (built here)
 # Every GPU step runs under its own time limit; the first failing step ends the call.
@@ -44,7 +45,10 @@ bench)
 interf)
     run interf_fused8 200 python tools/gather_interference.py fused 8
     run interf_fused8_wait 200 python tools/gather_interference.py fused 8 wait
-    run interf_fused8_nofence 200 env CTR_REACH_AMD_LIB=$LIBDIR/libab_nofence.so python tools/gather_interference.py fused 8
+    ;;
+profile)
+    bash scripts/profile.sh r04 > gpurun_out/profile_r04.log 2>&1 || { tail -5 gpurun_out/profile_r04.log; exit 1; }
+    tail -3 gpurun_out/profile_r04.log
     ;;
 traffic)
     run bench_base 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
@@ -60,7 +64,23 @@ fake)
         run fake_$1 200 python tools/gather_interference.py fake $2 $1
     done
     ;;
+ab)
+    # A/B of the default library against $AB (lib/ names, space-separated): bit-equality of the
+    # bench workload (40 steps + one FK with counters), then k_step timing, interleaved twice
+    # (the arrays go to /tmp on the box: gpurun merges at most 64 MiB of gpurun_out back)
+    run abits_base 300 python tools/ab_bits.py run /tmp/abits_base.npz
+    for v in $AB; do
+        run abits_$v 300 env CTR_REACH_AMD_LIB=$LIBDIR/$v python tools/ab_bits.py run /tmp/abits_$v.npz
+        TAILN=30 run abits_cmp_$v 60 python tools/ab_bits.py cmp /tmp/abits_base.npz /tmp/abits_$v.npz
+    done
+    for rep in 1 2; do
+        for v in libctr_reach_amd.so $AB; do
+            TAILN=3 run steps_${v}_$rep 200 env CTR_REACH_AMD_LIB=$LIBDIR/$v python tools/time_step_modes.py
+            run bench_${v}_$rep 300 env CTR_REACH_AMD_LIB=$LIBDIR/$v python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+        done
+    done
+    ;;
 *)
-    echo "usage: bash scripts/r4.sh suite|bench|interf|traffic|fake ..."; exit 2 ;;
+    echo "usage: bash scripts/r4.sh suite|bench|interf|profile|traffic|fake|ab ..."; exit 2 ;;
 esac
 done
