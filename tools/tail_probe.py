@@ -1,5 +1,5 @@
 """Experiment: k_step's launch time with E extra spinning workgroups of T ns appended to its grid
-(tools/experiments/tail_probe.sh -> libab_tail.so; CTR_TAIL_WG = E, CTR_TAIL_NS = T), 65 536 envs,
+(tools/experiments/tail_probe.sh -> libab_tail.so; scripts/gpu.sh tailprobe; CTR_TAIL_WG = E, CTR_TAIL_NS = T), 65 536 envs,
 compliant scipy RK45, auto-reset off, 32 launches after 64 untimed ones from a stepped state.
 usage: CTR_REACH_AMD_LIB=.../libab_tail.so CTR_TAIL_WG=E CTR_TAIL_NS=T python tools/tail_probe.py"""
 import os
