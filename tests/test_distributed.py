@@ -380,7 +380,7 @@ def test_push_gather_setup_failure_raises_on_every_rank():
 
 def _rows(n, rank, seq):
     """A rank's packed block of step seq in the stand-in tests (distinct per rank and step)."""
-    return (torch.arange(n * 4, dtype=torch.float32).reshape(n, 4) + 1000 * rank + 1e5 * seq).contiguous()
+    return (torch.arange(n * 4, dtype=torch.float32).reshape(n, 4) + 1000 * rank + 1e5 * (seq % 1024)).contiguous()
 
 
 def _flow_worker(rank, world, port, n, steps, mode, q):
@@ -392,18 +392,27 @@ def _flow_worker(rank, world, port, n, steps, mode, q):
         import time
         from ctr_reach_amd import distributed as D
         ops = _ShmCopyOps()
-        wait_prev = mode == "wait_prev"
+        wait_prev = mode in ("wait_prev", "wrap")
         g = D.PushGather(n, depth=3, engine="fused", ops=ops, spin_limit=20000, wait_prev=wait_prev)
         rng = np.random.default_rng(rank)
         views = []
-        for seq in range(1, steps + 1):
+        first = 1
+        if mode == "wrap":
+            # a history just below 2^32: every sequence word at first - 1, every release word at
+            # first - depth (what steps 1 .. first - 1 left); the device sees step numbers mod 2^32
+            first = (1 << 32) - 5
+            g.seqw.fill_(int(np.uint32((first - 1) & 0xFFFFFFFF).astype(np.int32)))
+            g.rel.fill_(int(np.uint32((first - g.depth) & 0xFFFFFFFF).astype(np.int32)))
+            g.pending = first - 1
+            dist.barrier()
+        for seq in range(first, first + steps):
             if wait_prev:
                 # ranks run free (no barrier): rank 0 fast, the last rank slow, the others jittered
                 time.sleep(0.0 if rank == 0 else (0.02 if rank == world - 1 else float(rng.uniform(0, 0.01))))
             cur, prev, prev_seq = g.step_args(seq)
             ops.fused_step(cur, prev, prev_seq, seq, _rows(n, rank, seq), wait_prev=wait_prev)
             g.stepped(seq)
-            if wait_prev and seq >= 2:
+            if wait_prev and seq >= first + 1:
                 # after step seq (its fused wait), the view of step seq - 1 is complete and stays
                 # valid until this rank launches step seq + 1: read it now, slowly
                 time.sleep(0.003)
@@ -423,7 +432,7 @@ def _flow_worker(rank, world, port, n, steps, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["wait_prev", "rank0_consumes"])
+@pytest.mark.parametrize("mode", ["wait_prev", "rank0_consumes", "wrap"])
 def test_push_gather_flow_control_free_running_ranks(mode):
     """The fused push's flow control (slot releases + the fused consumer wait, as k_step runs
     them, emulated on the CPU stand-in) with ranks that run free at different speeds -- every rank
@@ -443,8 +452,9 @@ def test_push_gather_flow_control_free_running_ranks(mode):
         assert p.exitcode == 0
     for rank, views, err in got:
         assert err == 0, (rank, err)
-        if mode == "wait_prev":
-            assert [s for s, _ in views] == list(range(1, steps))
+        if mode in ("wait_prev", "wrap"):
+            first = 1 if mode == "wait_prev" else (1 << 32) - 5
+            assert [s for s, _ in views] == list(range(first, first + steps - 1))
         else:
             assert [s for s, _ in views] == (list(range(1, steps + 1)) if rank == 0 else [])
         for s, v in views:

@@ -199,3 +199,58 @@ def test_push_gather_free_running_ranks_one_gpu(cuda, world):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     assert err == 0 and all(res), (res, err)
+
+
+def _stalled_worker(rank, world, port, n, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ctr_reach_amd import CtrReachVecEnv
+        from ctr_reach_amd import _abi
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        env = CtrReachVecEnv(n, device=dev, seed=5, env_base=rank * n, pack_outputs=True)
+        env.reset()
+        g = env.enable_gather("push", depth=3, spin_limit=2000)
+        errs = []
+        if rank == 0:
+            # rank 1 never steps: it never releases a slot, so from step depth + 1 on this rank's
+            # k_step waits for the release, gives up after spin_limit polls, and flags it
+            rng = np.random.default_rng(4)
+            for _ in range(5):
+                env.step(_acts(env, rng))
+                torch.cuda.synchronize()
+                errs.append(int(g.err.item()))
+            q.put(errs)
+        dist.barrier()
+        assert _abi.CTR_GATHER_E_RELEASE_TIMEOUT == 4
+        g.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_push_gather_unreleased_slot_times_out_without_hanging(cuda):
+    """A consumer that never steps never releases its slots: the producer's k_step stores after a
+    bounded wait and sets CTR_GATHER_E_RELEASE_TIMEOUT (steps 1-3 need no release: depth 3)."""
+    import torch.multiprocessing as mp
+    world, n = 2, 1024
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_stalled_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        errs = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    assert errs[:3] == [0, 0, 0], errs
+    assert errs[3] & 4 and errs[4] & 4, errs
