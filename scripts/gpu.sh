@@ -7,6 +7,7 @@
 #   evidence  every bench line: headline x2, 128 steps, float64 observations, configs[1] x2,
 #             configs[4], mixed systems 0-3
 #   soak      reset-pool soak (tools/soak_pool.py: pooled vs synchronous resets, bit-equal)
+#   pushsoak  fused-push flow-control soak: $WORLD free-running ranks on one GPU (tools/push_soak.py)
 #   interf    fused push into 8 blocks on one GPU: per-step cost with and without the fused wait
 #   profile   scripts/profile.sh $TAG (kernel trace + PMC passes; tools/summarize_profile.py $TAG here)
 #   traffic   k_step / k_refill FETCH_SIZE and WRITE_SIZE at the bench's --steps 20, with the
@@ -63,6 +64,9 @@ evidence)
 soak)
     run soak_pool 600 python tools/soak_pool.py
     ;;
+pushsoak)
+    TAILN=12 run push_soak 600 python tools/push_soak.py ${WORLD:-8} ${STEPS:-200}
+    ;;
 interf)
     run interf_fused8 200 python tools/gather_interference.py fused 8
     run interf_fused8_wait 200 python tools/gather_interference.py fused 8 wait
@@ -112,7 +116,7 @@ tailprobe)
     done
     ;;
 *)
-    echo "usage: bash scripts/gpu.sh suite|bench|evidence|soak|interf|profile|traffic|fake|refill|ab|pmcab|tailprobe ..."
+    echo "usage: bash scripts/gpu.sh suite|bench|evidence|soak|pushsoak|interf|profile|traffic|fake|refill|ab|pmcab|tailprobe ..."
     exit 2 ;;
 esac
 done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B baseline: build libctr_reach_amd.so of a git revision (default HEAD) from a copy of that
 # revision's sources into gym-ctr-reach_amd/ctr_reach_amd/lib/libab_<name>.so, so the working
-# tree's library can be timed against it (scripts/ab_lib.sh expects libab_prev.so).
+# tree's library can be timed against it (scripts/gpu.sh ab takes the names in $AB).
 # usage: bash tools/experiments/build_rev.sh [rev] [name]
 set -euo pipefail
 REV=${1:-HEAD}
