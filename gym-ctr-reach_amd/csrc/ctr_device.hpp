@@ -370,6 +370,74 @@ __device__ __forceinline__ void rhs_core(const SegPar &p, const Trig &t, const d
 }
 
 // ------------------------------------------------------------------------------------------
+// Tube levels (no y pre-curvature, compliant model).  Tube i is present on [beta_i, beta_i + L_i]
+// with beta_i <= 0, so along a backbone the present set only shrinks: level 3 (tube 2 present),
+// level 2 (tube 1 present, tube 2 absent), level 1 (tube 0 alone).  An absent tube has wx = g = 0
+// and a parked u_z = 0 (fk_lane), so at level 2 every term of rhs_core with alpha_2 is an exact
+// zero (only sin/cos(alpha_1 - alpha_0) is needed, u_z,2 and alpha_2 stay constant), and at level 1
+// u' = 0 and the frame turns about (wx_0, 0, u_z,0) with no trig at all.  The level-L forms below
+// drop those zero terms and give the same values as rhs_core (up to the sign of zero results, which
+// no later operation can turn into a non-zero difference); fk_lane runs an attempt at the highest
+// level any active lane of the wave needs.
+// ------------------------------------------------------------------------------------------
+// Trig at level LV < 3: 2 = sin/cos(alpha_1 - alpha_0) only; 1 = none.  Entries a level does not
+// compute are 0 (finite: a level-3 RHS of a lower-level lane multiplies them by exact zeros).
+template <int LV, bool CAREFUL>
+__device__ __forceinline__ Trig trig_lv(const double al[3])
+{
+    static_assert(LV == 1 || LV == 2, "level 3 is trig_of");
+    Trig t;
+    t.c20 = t.s20 = t.c21 = t.s21 = 0.0;
+    t.c10 = t.s10 = 0.0;
+    if constexpr (LV == 2) {
+        const double d10 = al[1] - al[0];
+        ctr_math::sincos_tab(d10, s_trig_tab, t.s10, t.c10);
+        if (CAREFUL && __builtin_expect(__ballot(ctr_math::sincos_needs_slow(d10)) != 0, 0) &&
+            ctr_math::sincos_needs_slow(d10)) {
+            const ctr_math::SinCos r = ctr_math::sincos_slow(d10);
+            t.s10 = r.s;
+            t.c10 = r.c;
+        }
+    }
+    return t;
+}
+
+// rhs_core<false> at level LV < 3 (see above).
+template <int LV>
+__device__ __forceinline__ void rhs_core_lv(const SegPar &p, const Trig &t, const double uz[3], const double R[9],
+                                            double duz[3], double dR[9])
+{
+    static_assert(LV == 1 || LV == 2, "level 3 is rhs_core");
+    if constexpr (LV == 2) {
+        const double sy1 = p.wx[1] * t.s10;              // rhs_core's sy1 with wx_2 = 0
+        const double sy2 = -(p.wx[0] * t.s10);
+        duz[0] = -(p.g[0] * sy1);
+        duz[1] = -(p.g[1] * sy2);
+        duz[2] = 0.0;
+        const double a = fma(p.wx[1], t.c10, p.wx[0]);
+        const double b = sy1;
+        const double u0 = uz[0];
+        #pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const double r0 = R[3 * r], r1 = R[3 * r + 1], r2 = R[3 * r + 2];
+            dR[3 * r + 0] = r1 * u0 - r2 * b;
+            dR[3 * r + 1] = r2 * a - r0 * u0;
+            dR[3 * r + 2] = r0 * b - r1 * a;
+        }
+    } else {
+        duz[0] = duz[1] = duz[2] = 0.0;
+        const double a = p.wx[0], u0 = uz[0];         // uy_0 = 0
+        #pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const double r0 = R[3 * r], r1 = R[3 * r + 1], r2 = R[3 * r + 2];
+            dR[3 * r + 0] = r1 * u0;
+            dR[3 * r + 1] = r2 * a - r0 * u0;
+            dR[3 * r + 2] = -(r1 * a);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // scipy RK45 (Dormand-Prince 5(4)) with scipy's step-size controller.
 // ------------------------------------------------------------------------------------------
 namespace rk {
@@ -475,6 +543,143 @@ __device__ __forceinline__ void stage_at(const SegPar &p, const Trig &t, const d
     rcol[0] = R[2]; rcol[1] = R[5]; rcol[2] = R[8];
 }
 
+
+// One attempt of RungeKutta._step_impl (rk.py:111-175) from y over h (tnew = t + h) at tube level
+// LV < 3 ("Tube levels"; no y pre-curvature, compliant model, no dense output): only the NU u_z and
+// NA alpha components the level changes are integrated -- the others keep y's value, their
+// derivatives and error terms being exact zeros -- and only the level's trig is evaluated.  Same
+// values as fk_lane's own (level-3) attempt for every lane at level LV or below; the error norm's
+// partial sums skip only +0 terms, in the same order.
+template <int LV, bool CAREFUL>
+__device__ __forceinline__ void rk45_attempt_lv(const SegPar &p, double yu[3], double ya[3], double yr[3],
+                                                double yR[9], Stage &f, Trig &ty, double &t, double tb, double &ha,
+                                                double h, double tnew, bool &rejected, bool &new_step,
+                                                bool &need_init, FkStats &st)
+{
+    using namespace rk;
+    static_assert(LV == 1 || LV == 2, "level 3 is fk_lane's own attempt");
+    constexpr int NU = LV == 2 ? 2 : 0;      // u_z components that change
+    constexpr int NA = LV == 2 ? 2 : 1;      // alpha components that change
+    constexpr int NT = LV == 2 ? 2 : 0;      // alpha stage inputs the trig reads
+#define CTR_FAL(i) ((i) == 0 ? (((p.present & 1u) != 0u) ? yu[0] : 0.0) : yu[i])
+    // f's implied parts: alpha' = masked u_z(y), r' = R(y) e3
+    const double fr[3] = {yR[2], yR[5], yR[8]};
+    double br[3], er[3];                     // B / E accumulators for r (never an RHS input)
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { br[i] = fr[i] * B0; er[i] = fr[i] * E0; }
+    Stage K1, K2, K3, K4, K5;
+    double ui[3], ai[3], Ri[9], rc[3];
+    // stage coefficients pre-multiplied by h: y + sum_j K_j (a_sj h)
+    const double a10 = A10 * h;
+    const double a20 = A20 * h, a21 = A21 * h;
+    const double a30 = A30 * h, a31 = A31 * h, a32 = A32 * h;
+    const double a40 = A40 * h, a41 = A41 * h, a42 = A42 * h, a43 = A43 * h;
+    const double a50 = A50 * h, a51 = A51 * h, a52 = A52 * h, a53 = A53 * h, a54 = A54 * h;
+    auto c1 = [&](double k0, double y) { return fma(k0, a10, y); };
+    auto c2 = [&](double k0, double k1, double y) { return fma(k1, a21, fma(k0, a20, y)); };
+    auto c3 = [&](double k0, double k1, double k2, double y) { return fma(k2, a32, fma(k1, a31, fma(k0, a30, y))); };
+    auto c4 = [&](double k0, double k1, double k2, double k3, double y) {
+        return fma(k3, a43, fma(k2, a42, fma(k1, a41, fma(k0, a40, y))));
+    };
+    auto c5 = [&](double k0, double k1, double k2, double k3, double k4, double y) {
+        return fma(k4, a54, fma(k3, a53, fma(k2, a52, fma(k1, a51, fma(k0, a50, y)))));
+    };
+#define CTR_STAGE(KOUT, EXPR_U, EXPR_A, EXPR_R, BCOEF, ECOEF)                                   \
+    {                                                                                          \
+        _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                        \
+            ui[i] = (i < NU) ? (EXPR_U) : yu[i];                                               \
+            if (i < NT) ai[i] = EXPR_A;                                                        \
+        }                                                                                      \
+        _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = EXPR_R;                          \
+        const Trig tt = trig_lv<LV, CAREFUL>(ai);                                              \
+        rhs_core_lv<LV>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                       \
+        stage_at<false>(p, tt, ui, Ri, KOUT, rc);                                              \
+        _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                        \
+            br[i] += rc[i] * (BCOEF);                                                          \
+            er[i] += rc[i] * (ECOEF);                                                          \
+        }                                                                                      \
+    }
+    CTR_STAGE(K1, c1(f.uz[i], yu[i]), c1(CTR_FAL(i), ya[i]), c1(f.R[i], yR[i]), 0.0, 0.0)
+    CTR_STAGE(K2, c2(f.uz[i], K1.uz[i], yu[i]), c2(CTR_FAL(i), K1.al[i], ya[i]), c2(f.R[i], K1.R[i], yR[i]), B2, E2)
+    CTR_STAGE(K3, c3(f.uz[i], K1.uz[i], K2.uz[i], yu[i]), c3(CTR_FAL(i), K1.al[i], K2.al[i], ya[i]),
+              c3(f.R[i], K1.R[i], K2.R[i], yR[i]), B3, E3)
+    CTR_STAGE(K4, c4(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], yu[i]), c4(CTR_FAL(i), K1.al[i], K2.al[i], K3.al[i], ya[i]),
+              c4(f.R[i], K1.R[i], K2.R[i], K3.R[i], yR[i]), B4, E4)
+    CTR_STAGE(K5, c5(f.uz[i], K1.uz[i], K2.uz[i], K3.uz[i], K4.uz[i], yu[i]),
+              c5(CTR_FAL(i), K1.al[i], K2.al[i], K3.al[i], K4.al[i], ya[i]),
+              c5(f.R[i], K1.R[i], K2.R[i], K3.R[i], K4.R[i], yR[i]), B5, E5)
+#undef CTR_STAGE
+    // y_new (rk.py rk_step) and the error sums without K6
+    double nu[3], na[3], nr[3], nR[9];
+    double eu[3], ea[3], eR[9];
+    const double b0 = B0 * h, b2 = B2 * h, b3 = B3 * h, b4 = B4 * h, b5 = B5 * h;
+    auto cb = [&](double k0, double k2, double k3, double k4, double k5, double y) {
+        return fma(k5, b5, fma(k4, b4, fma(k3, b3, fma(k2, b2, fma(k0, b0, y)))));
+    };
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        nu[i] = (i < NU) ? cb(f.uz[i], K2.uz[i], K3.uz[i], K4.uz[i], K5.uz[i], yu[i]) : yu[i];
+        na[i] = (i < NA) ? cb(CTR_FAL(i), K2.al[i], K3.al[i], K4.al[i], K5.al[i], ya[i]) : ya[i];
+        nr[i] = yr[i] + h * br[i];
+        eu[i] = (i < NU) ? f.uz[i] * E0 + K2.uz[i] * E2 + K3.uz[i] * E3 + K4.uz[i] * E4 + K5.uz[i] * E5 : 0.0;
+        ea[i] = (i < NA) ? CTR_FAL(i) * E0 + K2.al[i] * E2 + K3.al[i] * E3 + K4.al[i] * E4 + K5.al[i] * E5 : 0.0;
+    }
+    #pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        nR[i] = cb(f.R[i], K2.R[i], K3.R[i], K4.R[i], K5.R[i], yR[i]);
+        eR[i] = f.R[i] * E0 + K2.R[i] * E2 + K3.R[i] * E3 + K4.R[i] * E4 + K5.R[i] * E5;
+    }
+    Stage K6;
+    double k6r[3];
+    const Trig tn = trig_lv<LV, CAREFUL>(na);
+    rhs_core_lv<LV>(p, tn, nu, nR, K6.uz, K6.R);
+    stage_at<false>(p, tn, nu, nR, K6, k6r);
+    st.nfev += 6;
+    // error norm as fk_lane's attempt (three partial sums), without the +0 terms
+    double acc[3] = {0.0, 0.0, 0.0};
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (i < NU) {
+            const double xu = fma(K6.uz[i], E6, eu[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yu[i], nu[i]), RTOL, ATOL));
+            acc[0] = fma(xu, xu, acc[0]);
+        }
+        if (i < NA) {
+            const double xa = fma(K6.al[i], E6, ea[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(ya[i], na[i]), RTOL, ATOL));
+            acc[1] = fma(xa, xa, acc[1]);
+        }
+        const double xr = fma(k6r[i], E6, er[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yr[i], nr[i]), RTOL, ATOL));
+        acc[2] = fma(xr, xr, acc[2]);
+    }
+    #pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const double xR = fma(K6.R[i], E6, eR[i]) * ctr_math::rcp_est(fma(ctr_math::absmax(yR[i], nR[i]), RTOL, ATOL));
+        acc[i / 3] = fma(xR, xR, acc[i / 3]);
+    }
+    double en2 = (acc[0] + acc[1]) + acc[2];
+    en2 *= h * h;                           // = 18 error_norm^2
+    const double en2n = en2 * (1.0 / 18);   // error_norm^2
+    const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
+    if (en2n < 1.0) {
+        double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
+        if (rejected) factor = fmin(1.0, factor);
+        ha *= factor;
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) { yu[i] = nu[i]; ya[i] = na[i]; yr[i] = nr[i]; }
+        #pragma unroll
+        for (int i = 0; i < 9; ++i) yR[i] = nR[i];
+        f = K6;
+        ty = tn;
+        t = tnew;
+        st.nstep++;
+        new_step = true;
+        if (t - tb >= 0.0) need_init = true;    // segment finished (status 'finished')
+    } else {
+        ha *= fmax(0.2, fpow);
+        rejected = true;
+        st.nrej++;
+    }
+#undef CTR_FAL
+}
 
 // Forward kinematics of one lane, scipy-RK45 integrator: joints (f64; the env's float32 joints
 // promoted exactly as model.py:51 does) -> tip (f64).  RIGID: torsionally rigid variant (GJ -> inf:
@@ -701,6 +906,19 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         const double h = tnew - t;
         ha = fabs(h);
 
+        if constexpr (!HAS_UY && !RIGID && !SHAPE) {
+            // no active lane of the wave has tube 2 (level 3): the attempt at the wave's tube level
+            // ("Tube levels"); the level-3 attempt below stays as it is
+            if (__ballot((p.present & 4u) != 0) == 0) {
+                if (__ballot((p.present & 2u) != 0) != 0)
+                    rk45_attempt_lv<2, CAREFUL>(p, yu, ya, yr, yR, f, ty, t, tb, ha, h, tnew, rejected, new_step,
+                                                need_init, st);
+                else
+                    rk45_attempt_lv<1, CAREFUL>(p, yu, ya, yr, yR, f, ty, t, tb, ha, h, tnew, rejected, new_step,
+                                                need_init, st);
+                continue;
+            }
+        }
         // f's implied parts: alpha' = masked u_z(y), r' = R(y) e3
         double fr[3] = {yR[2], yR[5], yR[8]};
         // B / E accumulators for r (never an RHS input)
