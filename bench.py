@@ -376,7 +376,7 @@ def main():
                 backend_used = "rccl"
         # the env steps on a high-priority stream (RCCL's gather runs on its normal-priority one).
         # RCCL's gather kernel (248-256 VGPRs, 37 KB LDS per workgroup) cannot share a SIMD with a
-        # k_step wave (384 of the 512 registers), so whichever is dispatched first holds the CU:
+        # k_step wave (368 of the 512 registers), so whichever is dispatched first holds the CU:
         # with the step first, the gather of step t fills the CUs the slowest waves of step t+1
         # leave idle instead of keeping step t+1's workgroups off the CUs it took
         hp = torch.cuda.Stream(device=dev, priority=-1)

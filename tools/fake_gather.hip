@@ -1,7 +1,7 @@
 // Stand-in for RCCL's all-gather kernel on one GPU (tools/gather_interference.py): workgroups
 // with the device kernel's footprint (ncclDevKernel_Generic_* in librccl 7.2, gfx950: 256 VGPRs,
 // 37.7 KB LDS, 256 lanes) that stay resident for a fixed number of shader-clock cycles, so the
-// dispatch interplay with k_step (one 384-register wave per SIMD) can be timed without 8 GPUs.
+// dispatch interplay with k_step (one 368-register wave per SIMD) can be timed without 8 GPUs.
 // Build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC tools/fake_gather.hip -o tools/libfake_gather.so
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -16,7 +16,7 @@ b32 moves), and each lane forms its row of R [u]x (6 ops).  Per attempt each lan
 Today's counts come from the census of the level-3 attempt block (1 117-1 153 instructions).
 
 Time model: every VALU instruction of a wave64 occupies its SIMD for 4 cycles (16 lanes per cycle,
-FP64 FMA at full rate); one wave per SIMD (today: 384 registers per lane) issues one instruction
+FP64 FMA at full rate); one wave per SIMD (today: 368 registers per lane) issues one instruction
 per 5.15 cycles on average (PMC, profiles/r03c_pmc.json: its dependent FP64 chains), while >= 2
 waves per SIMD fill the pipe (4 cycles per instruction).  The iterations per wave come from the
 CPU oracle's per-segment attempt counts on env-trajectory joints (tools/sim_sched.py's wave
