@@ -659,25 +659,32 @@ __device__ __forceinline__ void rk45_attempt_lv(const SegPar &p, double yu[3], d
     en2 *= h * h;                           // = 18 error_norm^2
     const double en2n = en2 * (1.0 / 18);   // error_norm^2
     const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
-    if (en2n < 1.0) {
-        double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
-        if (rejected) factor = fmin(1.0, factor);
-        ha *= factor;
-        #pragma unroll
-        for (int i = 0; i < 3; ++i) { yu[i] = nu[i]; ya[i] = na[i]; yr[i] = nr[i]; }
-        #pragma unroll
-        for (int i = 0; i < 9; ++i) yR[i] = nR[i];
-        f = K6;
-        ty = tn;
-        t = tnew;
-        st.nstep++;
-        new_step = true;
-        if (t - tb >= 0.0) need_init = true;    // segment finished (status 'finished')
-    } else {
-        ha *= fmax(0.2, fpow);
-        rejected = true;
-        st.nrej++;
+    // accept / reject as selects (fk_lane's attempt does the same)
+    const bool ok = en2n < 1.0;
+    double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
+    if (rejected) factor = fmin(1.0, factor);
+    ha *= ok ? factor : fmax(0.2, fpow);
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (i < NU) yu[i] = ok ? nu[i] : yu[i];
+        if (i < NA) ya[i] = ok ? na[i] : ya[i];
+        yr[i] = ok ? nr[i] : yr[i];
     }
+    #pragma unroll
+    for (int i = 0; i < 9; ++i) yR[i] = ok ? nR[i] : yR[i];
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { f.uz[i] = ok ? K6.uz[i] : f.uz[i]; f.al[i] = ok ? K6.al[i] : f.al[i]; }
+    #pragma unroll
+    for (int i = 0; i < 9; ++i) f.R[i] = ok ? K6.R[i] : f.R[i];
+    ty.c10 = ok ? tn.c10 : ty.c10; ty.s10 = ok ? tn.s10 : ty.s10;
+    ty.c20 = ok ? tn.c20 : ty.c20; ty.s20 = ok ? tn.s20 : ty.s20;
+    ty.c21 = ok ? tn.c21 : ty.c21; ty.s21 = ok ? tn.s21 : ty.s21;
+    t = ok ? tnew : t;
+    st.nstep += ok ? 1u : 0u;
+    st.nrej += ok ? 0u : 1u;
+    new_step = ok;
+    rejected = ok ? rejected : true;
+    if (ok && t - tb >= 0.0) need_init = true;    // segment finished (status 'finished')
 #undef CTR_FAL
 }
 
@@ -1029,7 +1036,34 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         // error_norm ** -0.2 = (error_norm^2) ** -0.1
         const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
         CTR_STAMP(ts3);
-        if (en2n < 1.0) {
+        if constexpr (!SHAPE) {
+            // accept / reject as selects: both paths would run in most iterations of a wave anyway
+            const bool ok = en2n < 1.0;
+            double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
+            if (rejected) factor = fmin(1.0, factor);
+            ha *= ok ? factor : fmax(0.2, fpow);
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                yu[i] = ok ? nu[i] : yu[i];
+                ya[i] = ok ? na[i] : ya[i];
+                yr[i] = ok ? nr[i] : yr[i];
+            }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) yR[i] = ok ? nR[i] : yR[i];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) { f.uz[i] = ok ? K6.uz[i] : f.uz[i]; f.al[i] = ok ? K6.al[i] : f.al[i]; }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) f.R[i] = ok ? K6.R[i] : f.R[i];
+            ty.c10 = ok ? tn.c10 : ty.c10; ty.s10 = ok ? tn.s10 : ty.s10;
+            ty.c20 = ok ? tn.c20 : ty.c20; ty.s20 = ok ? tn.s20 : ty.s20;
+            ty.c21 = ok ? tn.c21 : ty.c21; ty.s21 = ok ? tn.s21 : ty.s21;
+            t = ok ? tnew : t;
+            st.nstep += ok ? 1u : 0u;
+            st.nrej += ok ? 0u : 1u;
+            new_step = ok;
+            rejected = ok ? rejected : true;
+            if (ok && t - tb >= 0.0) need_init = true;    // segment finished (status 'finished')
+        } else if (en2n < 1.0) {
             double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
             ha *= factor;
