@@ -893,7 +893,7 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         // ---- one attempt of RungeKutta._step_impl (rk.py:111-175) ----
         {
             // new step: min_step = 10 |nextafter(t, inf) - t| and h_abs >= min_step (rk.py:114-119)
-            const double ms = 10.0 * fabs(nextafter(t, INFINITY) - t);
+            const double ms = 10.0 * ctr_math::gap_up(t);       // = 10 |nextafter(t, inf) - t|
             min_step = new_step ? ms : min_step;
             ha = (new_step && ha < ms) ? ms : ha;
             rejected = new_step ? false : rejected;

@@ -197,8 +197,8 @@ CTR_HD double inv_root10(double x)
     int e;
     const double m = frexp(x, &e);                       // x = m 2^e, m in [0.5, 1)
     // write e - 1 = 10 k + r with r in [0, 10)
-    const int em1 = e - 1;
-    const int k = (em1 >= 0) ? em1 / 10 : -((9 - em1) / 10);
+    const int em1 = e - 1;                               // >= -1075 (subnormals), so em1 + 1100 >= 0:
+    const int k = (int)((unsigned)(em1 + 1100) / 10u) - 110;   // floor((e - 1) / 10), no branch
     const int r = em1 - 10 * k;
     const double xs = ldexp(m, r + 1);                   // x' = x 2^(-10k) in [1, 2^10)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -214,6 +214,21 @@ CTR_HD double inv_root10(double x)
         y = y + y * ((1.0 - t) * 0.1);                   // y (1 + (1 - t)/10)
     }
     return ldexp(y, -k);
+}
+
+// nextafter(t, +inf) - t, exactly, without nextafter's integer bit manipulation (a power of two:
+// 2^(e-53) for |t| = m 2^e, m in [0.5, 1), half that for a negative power of two, 2^-1074 at and
+// below the subnormal spacing); NaN for NaN and +inf, +inf for -inf and the largest double, as
+// nextafter(t, inf) - t.
+CTR_HD double gap_up(double t)
+{
+    int e;
+    const double m = frexp(t, &e);
+    const int sh = (m == -0.5) ? 54 : 53;
+    const int p = e - sh;
+    double g = ldexp(1.0, p < -1074 ? -1074 : p);
+    g = (t == 0.0) ? 4.9406564584124654e-324 : g;
+    return (t == -INFINITY || t == 1.7976931348623157e308) ? INFINITY : g + 0.0 * t;
 }
 
 // sqrt(x) for finite x > 0, ~1 ulp: reciprocal square root estimate + Newton (no division).

@@ -108,3 +108,38 @@ def test_sampler_round_tables():
         for rank in range(k):
             want = sum(1 << i for i in range(rank, 64, k))
             assert (stride << rank) & ((1 << 64) - 1) == want, (k, rank)
+
+
+def test_gap_up_matches_nextafter(tmp_path):
+    """ctr_math::gap_up(t) == nextafter(t, inf) - t bit for bit (the RK45 min_step, rk.py:114-119):
+    normals, subnormals, signed zeros, negative powers of two (where the gap toward zero halves),
+    the extremes and non-finite values."""
+    src = tmp_path / "m3.cpp"
+    src.write_text('#include "ctr_math.hpp"\n'
+                   'extern "C" void vgap(const double* x, double* y, long n) {\n'
+                   '  for (long i = 0; i < n; ++i) y[i] = ctr_math::gap_up(x[i]); }\n')
+    so = tmp_path / "m3.so"
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-shared", "-fPIC",
+                           "-I", os.path.join(ROOT, "gym-ctr-reach_amd", "csrc"), str(src), "-o", str(so)])
+    lib = ctypes.CDLL(str(so))
+    lib.vgap.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_long]
+    rng = np.random.default_rng(2)
+    p2 = np.ldexp(1.0, np.arange(-1074, 1024))
+    x = np.concatenate([rng.uniform(-1, 1, 100000), rng.uniform(0, 0.6, 100000),
+                        10.0 ** rng.uniform(-320, 308, 100000) * rng.choice([-1.0, 1.0], 100000),
+                        p2, -p2, np.nextafter(p2, 0), -np.nextafter(p2, 0), np.nextafter(p2, np.inf),
+                        np.array([0.0, -0.0, 5e-324, -5e-324, 1.7976931348623157e308,
+                                  -1.7976931348623157e308, np.inf, -np.inf, np.nan])])
+    y = np.empty_like(x)
+    with np.errstate(invalid="ignore", over="ignore"):
+        want = np.nextafter(x, np.inf) - x
+    lib.vgap(x.ctypes.data, y.ctypes.data, len(x))
+    same = (y.view(np.uint64) == want.view(np.uint64)) | (np.isnan(y) & np.isnan(want))
+    assert same.all(), (x[~same][:5], y[~same][:5], want[~same][:5])
+
+
+def test_inv_root10_exponent_split():
+    """inv_root10's branch-free k = floor((e - 1) / 10) over every frexp exponent of a double."""
+    for e in range(-1075, 1026):
+        em1 = e - 1
+        assert ((em1 + 1100) // 10) - 110 == em1 // 10, e
