@@ -658,7 +658,9 @@ __device__ __forceinline__ void rk45_attempt_lv(const SegPar &p, double yu[3], d
     double en2 = (acc[0] + acc[1]) + acc[2];
     en2 *= h * h;                           // = 18 error_norm^2
     const double en2n = en2 * (1.0 / 18);   // error_norm^2
-    const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
+    // unguarded: for en2n >= 1e300 (or inf / NaN) the root is < 2e-30 (or NaN) and only enters
+    // fmax(0.2, fpow) of a rejection, which is 0.2 either way (rk.py:171)
+    const double fpow = 0.9 * ctr_math::inv_root10(en2n);
     // accept / reject as selects (fk_lane's attempt does the same)
     const bool ok = en2n < 1.0;
     double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
@@ -1034,7 +1036,9 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         en2 *= h * h;                       // = 18 error_norm^2
         const double en2n = en2 * (1.0 / 18);   // error_norm^2
         // error_norm ** -0.2 = (error_norm^2) ** -0.1
-        const double fpow = (en2n < 1e300) ? 0.9 * ctr_math::inv_root10(en2n) : 0.0;
+        // unguarded: for en2n >= 1e300 (or inf / NaN) the root is < 2e-30 (or NaN) and only enters
+        // fmax(0.2, fpow) of a rejection, which is 0.2 either way (rk.py:171)
+        const double fpow = 0.9 * ctr_math::inv_root10(en2n);
         CTR_STAMP(ts3);
         if constexpr (!SHAPE) {
             // accept / reject as selects: both paths would run in most iterations of a wave anyway

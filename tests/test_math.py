@@ -143,3 +143,16 @@ def test_inv_root10_exponent_split():
     for e in range(-1075, 1026):
         em1 = e - 1
         assert ((em1 + 1100) // 10) - 110 == em1 // 10, e
+
+
+def test_inv_root10_unguarded_tail(tmp_path):
+    """The RK45 step factor is 0.9 inv_root10(err^2) without a guard (ctr_device.hpp): for a huge,
+    infinite or NaN err^2 it must stay below 0.2 or be NaN, so that a rejection's fmax(0.2, .)
+    gives 0.2 as rk.py:171 does for an infinite norm."""
+    lib = _lib2(tmp_path)
+    x = np.array([1e300, 3e300, 1e305, 1.7976931348623157e308, np.inf, np.nan])
+    y = np.empty_like(x)
+    lib.vir10(x.ctypes.data, y.ctypes.data, len(x))
+    f = 0.9 * y
+    assert np.all(np.isnan(f) | (f < 0.2)), f
+    assert np.all(np.fmax(0.2, f) == 0.2)
