@@ -871,11 +871,26 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
     }
 }
 
+#if defined(CTR_DIAG_WAVETIME)
+// timing diagnostic only (tools/wave_times.py): each wave's start and end on the 100 MHz clock
+__device__ unsigned long long g_diag_wave_t[8192][2];
+#endif
+
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
                                                    ctr_step_out_t o, int32_t autoreset)
 {
+#if defined(CTR_DIAG_WAVETIME)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     step_body<MODE, false>(kc, b, actions, o, autoreset, HerK{});
+#if defined(CTR_DIAG_WAVETIME)
+    const int w = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);
+    if ((threadIdx.x & 63) == 0 && w < 8192) {
+        g_diag_wave_t[w][0] = t0;
+        g_diag_wave_t[w][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 template <int MODE>
@@ -1626,6 +1641,16 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
 }
 
 }  // namespace
+
+#if defined(CTR_DIAG_WAVETIME)
+extern "C" int ctr_diag_wavetimes(unsigned long long *dst, int n)
+{
+    if (!dst || n < 0 || n > 8192) return fail(CTR_EINVAL, "ctr_diag_wavetimes: bad arguments");
+    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_diag_wave_t), (size_t)n * 16, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return hip_check("ctr_diag_wavetimes");
+    return 0;
+}
+#endif
 
 extern "C" {
 

@@ -18,6 +18,8 @@
 #   ab        A/B of the default library against the libraries named in $AB (file names under
 #             gym-ctr-reach_amd/ctr_reach_amd/lib, e.g. built by tools/experiments/build_rev.sh):
 #             bit-equality of the bench workload, then k_step timing and the headline, interleaved
+#   abt       k_step timing only, default library and each of $AB (diagnostic builds)
+#   wavet     per-wave k_step durations (libab_wavet.so, -DCTR_DIAG_WAVETIME; tools/wave_times.py)
 #   pmcab     PMC passes per library in $AB and the default one (scripts/pmc_ab.sh $TAG ...)
 #   tailprobe k_step with extra spinning workgroups (libab_tail.so, tools/experiments/tail_probe.sh)
 # Every GPU step runs under its own time limit; the first failing step ends the call.
@@ -106,6 +108,16 @@ ab)
         done
     done
     ;;
+abt)
+    # timing only (diagnostic builds whose results differ, e.g. -DCTR_DIAG_NOFK): k_step per library
+    for v in libctr_reach_amd.so $AB; do
+        TAILN=3 run steps_${v} 200 env CTR_REACH_AMD_LIB=$LIBDIR/$v python tools/time_step_modes.py
+    done
+    ;;
+wavet)
+    # per-wave durations of k_step (libab_wavet.so, built with -DCTR_DIAG_WAVETIME; tools/wave_times.py)
+    TAILN=3 run wave_times 200 env CTR_REACH_AMD_LIB=$LIBDIR/libab_wavet.so python tools/wave_times.py
+    ;;
 pmcab)
     bash scripts/pmc_ab.sh ${TAG:-ab} libctr_reach_amd.so $AB || exit 1
     ;;
@@ -116,7 +128,7 @@ tailprobe)
     done
     ;;
 *)
-    echo "usage: bash scripts/gpu.sh suite|bench|evidence|soak|pushsoak|interf|profile|traffic|fake|refill|ab|pmcab|tailprobe ..."
+    echo "usage: bash scripts/gpu.sh suite|bench|evidence|soak|pushsoak|interf|profile|traffic|fake|refill|ab|abt|wavet|pmcab|tailprobe ..."
     exit 2 ;;
 esac
 done

@@ -1,0 +1,53 @@
+"""Diagnostic: the duration of every k_step wave of one launch, from a library built with
+-DCTR_DIAG_WAVETIME (each wave's lane 0 stores its start and end on the 100 MHz real-time clock).
+Is the launch as long as its slowest wave with the others close behind (per-iteration cost is the
+lever), or do a few waves trail the rest (work balance is)?
+
+build: make -C gym-ctr-reach_amd HIPFLAGS="<the Makefile's flags> -DCTR_DIAG_WAVETIME" \\
+           LIB=ctr_reach_amd/lib/libab_wavet.so ctr_reach_amd/lib/libab_wavet.so
+usage: CTR_REACH_AMD_LIB=.../libab_wavet.so python tools/wave_times.py [n_envs]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+from ctr_reach_amd import CtrReachVecEnv, _abi  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+env = CtrReachVecEnv(n, device="cuda", seed=0, refill_interval=64)
+env.reset()
+lib = env.lib
+lib.ctr_diag_wavetimes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+g = torch.Generator(device="cuda")
+g.manual_seed(1)
+hi = torch.tensor(env.action_space.high, device="cuda")
+acts = [((torch.rand((n, 6), generator=g, device="cuda") * 2 - 1) * hi).contiguous() for _ in range(8)]
+g0 = torch.Generator(device="cpu")
+g0.manual_seed(2)
+env.t.copy_(torch.randint(0, 150, (n,), generator=g0, dtype=torch.int32))
+stream = torch.cuda.current_stream()
+sp = _abi.stream_ptr(stream)
+nw = n // 64
+rows = []
+for mode, name in ((0, "autoreset off"), (_abi.AUTORESET_POOLED, "pooled auto-reset")):
+    for i in range(300):
+        _abi.check(lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[i % 8]), env._out, mode, sp), "ctr_step")
+        if mode and i % 32 == 31:
+            env.refill_pool()
+    durs, spans = [], []
+    for rep in range(8):
+        _abi.check(lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[rep % 8]), env._out, mode, sp), "ctr_step")
+        torch.cuda.synchronize()
+        t = np.zeros((nw, 2), dtype=np.uint64)
+        _abi.check(lib.ctr_diag_wavetimes(t.ctypes.data, nw), "ctr_diag_wavetimes")
+        d = (t[:, 1] - t[:, 0]).astype(np.float64) * 0.01          # us
+        durs.append(d)
+        spans.append((t[:, 1].max() - t[:, 0].min()) * 0.01)
+    d = np.concatenate(durs)
+    q = np.percentile(d, [0, 10, 50, 90, 99, 100])
+    print("%-18s wave us: min %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f mean %.1f | launch span %.1f us "
+          "| mean/max %.3f" % (name, *q, d.mean(), float(np.mean(spans)), d.mean() / q[-1]), flush=True)
