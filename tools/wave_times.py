@@ -1,5 +1,7 @@
 """Diagnostic: the duration of every k_step wave of one launch, from a library built with
--DCTR_DIAG_WAVETIME (each wave's lane 0 stores its start and end on the 100 MHz real-time clock).
+-DCTR_DIAG_WAVETIME (each wave's lane 0 stores the kernel's start, the FK's start and end, the finish's and the appends'
+end, and the kernel's end on the
+100 MHz real-time clock).
 Is the launch as long as its slowest wave with the others close behind (per-iteration cost is the
 lever), or do a few waves trail the rest (work balance is)?
 
@@ -38,16 +40,31 @@ for mode, name in ((0, "autoreset off"), (_abi.AUTORESET_POOLED, "pooled auto-re
         _abi.check(lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[i % 8]), env._out, mode, sp), "ctr_step")
         if mode and i % 32 == 31:
             env.refill_pool()
-    durs, spans = [], []
+    durs, spans, pre, fk, post, st0, fin, app, end = [], [], [], [], [], [], [], [], []
     for rep in range(8):
         _abi.check(lib.ctr_step(env.cfg, env._batch, _abi.ptr(acts[rep % 8]), env._out, mode, sp), "ctr_step")
         torch.cuda.synchronize()
-        t = np.zeros((nw, 2), dtype=np.uint64)
+        t = np.zeros((nw, 6), dtype=np.uint64)
         _abi.check(lib.ctr_diag_wavetimes(t.ctypes.data, nw), "ctr_diag_wavetimes")
-        d = (t[:, 1] - t[:, 0]).astype(np.float64) * 0.01          # us
+        d = (t[:, 5] - t[:, 0]).astype(np.float64) * 0.01          # us
         durs.append(d)
-        spans.append((t[:, 1].max() - t[:, 0].min()) * 0.01)
+        pre.append((t[:, 1] - t[:, 0]).astype(np.float64) * 0.01)
+        fk.append((t[:, 2] - t[:, 1]).astype(np.float64) * 0.01)
+        post.append((t[:, 5] - t[:, 2]).astype(np.float64) * 0.01)
+        fin.append((t[:, 3] - t[:, 2]).astype(np.float64) * 0.01)
+        app.append((t[:, 4] - t[:, 3]).astype(np.float64) * 0.01)
+        end.append((t[:, 5] - t[:, 4]).astype(np.float64) * 0.01)
+        st0.append((t[:, 0] - t[:, 0].min()).astype(np.float64) * 0.01)
+        spans.append((t[:, 5].max() - t[:, 0].min()) * 0.01)
     d = np.concatenate(durs)
     q = np.percentile(d, [0, 10, 50, 90, 99, 100])
     print("%-18s wave us: min %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f mean %.1f | launch span %.1f us "
           "| mean/max %.3f" % (name, *q, d.mean(), float(np.mean(spans)), d.mean() / q[-1]), flush=True)
+    for lab, arr in (("start skew", st0), ("pre-FK", pre), ("FK", fk), ("post-FK", post), ("  finish", fin),
+                     ("  appends", app), ("  to end", end)):
+        a = np.concatenate(arr)
+        print("    %-10s us: p50 %.2f p90 %.2f max %.2f mean %.2f" % (lab, *np.percentile(a, [50, 90, 100]), a.mean()),
+              flush=True)
+    sl = int(np.argmax(durs[0]))
+    print("    slowest wave of launch 0: #%d  pre %.2f FK %.2f post %.2f start %.2f" % (
+        sl, pre[0][sl], fk[0][sl], post[0][sl], st0[0][sl]), flush=True)
