@@ -116,7 +116,7 @@ abt)
     ;;
 wavet)
     # per-wave durations of k_step (libab_wavet.so, built with -DCTR_DIAG_WAVETIME; tools/wave_times.py)
-    TAILN=18 run wave_times 200 env CTR_REACH_AMD_LIB=$LIBDIR/libab_wavet.so python tools/wave_times.py
+    TAILN=20 run wave_times 200 env CTR_REACH_AMD_LIB=$LIBDIR/libab_wavet.so python tools/wave_times.py
     ;;
 pmcab)
     bash scripts/pmc_ab.sh ${TAG:-ab} libctr_reach_amd.so $AB || exit 1

@@ -65,6 +65,13 @@ for mode, name in ((0, "autoreset off"), (_abi.AUTORESET_POOLED, "pooled auto-re
         a = np.concatenate(arr)
         print("    %-10s us: p50 %.2f p90 %.2f max %.2f mean %.2f" % (lab, *np.percentile(a, [50, 90, 100]), a.mean()),
               flush=True)
+    # does the previous launch predict the slow waves?  (consecutive launches of the same envs)
+    cor = np.mean([np.corrcoef(durs[k], durs[k + 1])[0, 1] for k in range(len(durs) - 1)])
+    top = np.mean([len(set(np.argsort(durs[k])[-16:]) & set(np.argsort(durs[k + 1])[-16:])) / 16.0
+                   for k in range(len(durs) - 1)])
+    rank = np.mean([int((durs[k] > durs[k][int(np.argmax(durs[k + 1]))]).sum()) for k in range(len(durs) - 1)])
+    print("    consecutive launches: duration correlation %.3f, top-16 overlap %.2f, the next slowest wave's "
+          "rank in this launch %.1f (0 = slowest)" % (cor, top, rank), flush=True)
     sl = int(np.argmax(durs[0]))
     print("    slowest wave of launch 0: #%d  pre %.2f FK %.2f post %.2f start %.2f" % (
         sl, pre[0][sl], fk[0][sl], post[0][sl], st0[0][sl]), flush=True)
