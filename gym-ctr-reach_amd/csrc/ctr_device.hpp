@@ -1048,7 +1048,9 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         const double fpow = 0.9 * ctr_math::inv_root10(en2n);
         CTR_STAMP(ts3);
         if constexpr (!SHAPE) {
-            // accept / reject as selects: both paths would run in most iterations of a wave anyway
+            // accept / reject (rk.py:160-175) as selects: in most iterations some lanes of a wave
+            // accept and some reject, so an if / else ran both sides, each copying the loop-carried
+            // state into the join's registers (DESIGN.md 4.5 log: -1.3 us, bit-equal)
             const bool ok = en2n < 1.0;
             double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
