@@ -227,21 +227,31 @@ CONFIGS = {
 
 
 def fk_work(env, joints):
-    """Algorithmic FP64 flops + sincos of one FK per env at the given joints (device counters)."""
+    """Algorithmic FP64 flops + sincos of one FK per env at the given joints (device counters).
+    Fixed-step RK4 (both models): stats nstep counts the steps taken stage by stage and nrej packs
+    the segments run as segment maps (bits 16-31) and their compositions (bits 0-15); a mapped
+    segment is priced at its EXECUTED work (the map, its compositions, its application to [R | r]),
+    not at the stepped RK4 count it replaces (nfev still reports 4 per RK4 step for parity)."""
     _, st = env.forward_kinematics(joints, env.system, return_stats=True)
     nfev = st["nfev"].double()
-    att = (st["nstep"] + st["nrej"]).double()
     seg = st["nseg"].double()
-    if env.integrator == "rk4" and env.model == "rigid":
-        # k_fk's stats[2] counts the square-and-multiply compositions; k_step's 8-lane groups
-        # run the same powers and join the segment maps in RIGID_TREE more compositions
-        per = seg * FLOP_RIGID_MAP + st["nrej"].double() * FLOP_COMPOSE + RIGID_TREE * FLOP_TREE
-    elif env.integrator == "rk4":
-        per = nfev * FLOP_RHS + att * FLOP_RK4_STEP
+    if env.integrator == "rk4":
+        nrej = st["nrej"].long()
+        maps, comps = (nrej >> 16).double(), (nrej & 0xFFFF).double()
+        stepped = st["nstep"].double()
+        rhs = 4 * stepped
+        if env.model == "rigid":
+            # k_step's 8-lane groups build the same maps and join them in RIGID_TREE compositions
+            per = maps * FLOP_RIGID_MAP + comps * FLOP_COMPOSE + RIGID_TREE * FLOP_TREE
+        else:
+            # stepped gaps at the SURVEY 8(d) count; the tube-0-alone tail as maps applied to [R | r]
+            per = rhs * FLOP_RHS + stepped * FLOP_RK4_STEP + maps * (FLOP_RIGID_MAP + FLOP_TREE) + comps * FLOP_COMPOSE
     else:
+        rhs = nfev
+        att = (st["nstep"] + st["nrej"]).double()
         per = nfev * FLOP_RHS + att * FLOP_ATTEMPT + seg * FLOP_SEGMENT
     flops = per.sum().item() + FLOP_STEP_EXTRA * joints.shape[0]
-    sincos = (nfev * SINCOS_RHS).sum().item()
+    sincos = (rhs * SINCOS_RHS).sum().item()
     return flops, sincos, nfev.mean().item()
 
 
@@ -624,7 +634,11 @@ def main():
                               ("the EXECUTED work of the rigid segment-power path (125 flop per segment map, 37 per "
                                "W-polynomial composition, 63 per 3x4 composition of the 8-lane group product), not the "
                                "stepped RK4 count"
-                               if cfgd["model"] == "rigid" else "SURVEY 8(d) count"))},
+                               if cfgd["model"] == "rigid" else
+                               "SURVEY 8(d) count for the RK4 steps taken stage by stage (4 RHS x 102 + 252 per step); the "
+                               "tube-0-alone tail segments run as segment maps and are priced at their EXECUTED work (125 "
+                               "per map + 63 to apply it + 37 per composition), not at the stepped count"
+                               if cfgd["integrator"] == "rk4" else "SURVEY 8(d) count"))},
     }
     tr = os.path.join(ROOT, "profiles", "traffic.json")
     if ws > 1:

@@ -493,8 +493,10 @@ __device__ __forceinline__ void shape_put(ShapeOut *so, double s, const double r
     so->count++;
 }
 
-// nrej: rejected RK45 attempts; fixed-step RK4 never rejects, so with the rigid model (whose
-// segments run as matrix powers) it counts the map compositions of square-and-multiply.
+// nrej: rejected RK45 attempts.  Fixed-step RK4 never rejects; there it counts the segments run as
+// segment maps (matrix powers: every segment of the rigid model, the tube-0-alone tail of the
+// compliant one) in bits 16-31 and their square-and-multiply compositions in bits 0-15, and
+// nstep counts only the steps taken stage by stage (nfev still counts 4 per RK4 step, mapped or not).
 struct FkStats {
     uint32_t nfev, nstep, nrej, nseg, status;
 };
@@ -1126,7 +1128,9 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
 // Fixed-step classical RK4 of the same ODE (throughput / convergence mode, BASELINE configs 2
 // and 5).  Each kept segment span [t0, tb] (the same spans as the RK45 path) is split into
 // n = max(1, ceil((tb - t0) * steps_per_m)) equal steps.  Lanes stay in lock-step: one loop
-// iteration = one RK4 step of whichever segment the lane is in.
+// iteration = one RK4 step of whichever segment the lane is in, at the wave's tube level; the
+// segments of constant curvature (all of them for the rigid model, the trailing tube-0-alone ones
+// for the compliant model) run afterwards as segment maps (fk_lane_rk4).
 // ------------------------------------------------------------------------------------------
 // Torsionally rigid model: u_z stays 0 and the tube angles keep their joint values, so on a
 // segment the curvature u is constant and the ODE is linear, Y' = Y A with Y = [[R, r], [0, 1]]
@@ -1221,12 +1225,128 @@ __device__ __forceinline__ int rigid_segment_map(const SegPar &p, const Trig &t,
     return ncomp;
 }
 
+// One classical RK4 step of the compliant model over h at tube level LV ("Tube levels": 3 = the
+// full RHS; 2 = tube 2 absent, so u_z,2 and alpha_2 keep their values -- their derivatives are
+// exact zeros, alpha' being masked by presence -- and only sin/cos(alpha_1 - alpha_0) is needed).
+// The level-2 form gives rhs_core's values up to the sign of zero results, so a lane at level 2
+// gets the same bits from either form; a wave runs the highest level one of its active lanes needs.
+template <int LV, bool HAS_UY, bool CAREFUL>
+__device__ __forceinline__ void rk4_step(const SegPar &p, double h, double yu[3], double ya[3], double yr[3],
+                                         double yR[9])
+{
+    static_assert(LV == 2 || LV == 3, "level 1 runs in closed form (rk4_tail_maps)");
+    static_assert(LV == 3 || !HAS_UY, "tube levels assume no y pre-curvature");
+    constexpr int N = LV == 3 ? 3 : 2;          // u_z / alpha components that change
+    auto rhs = [&](const double u[3], const double a[3], const double R[9], Stage &k, double rc[3]) {
+        if constexpr (LV == 3) {
+            const Trig tt = trig_of<CAREFUL>(a);
+            rhs_core<HAS_UY>(p, tt, u, R, k.uz, k.R);
+            stage_at(p, tt, u, R, k, rc);
+        } else {
+            const Trig tt = trig_lv<2, CAREFUL>(a);
+            rhs_core_lv<2>(p, tt, u, R, k.uz, k.R);
+            stage_at(p, tt, u, R, k, rc);
+        }
+    };
+    Stage k1, k2, k3, k4;
+    double r1[3], r2[3], r3[3], r4[3];
+    double ui[3], ai[3], Ri[9];
+    rhs(yu, ya, yR, k1, r1);
+    const double h2 = 0.5 * h;
+#define CTR_RK4_STAGE(KIN, KOUT, ROUT, C)                                                      \
+    {                                                                                          \
+        _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                        \
+            ui[i] = (i < N) ? fma(KIN.uz[i], C, yu[i]) : yu[i];                                \
+            ai[i] = (i < N) ? fma(KIN.al[i], C, ya[i]) : ya[i];                                \
+        }                                                                                      \
+        _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = fma(KIN.R[i], C, yR[i]);         \
+        rhs(ui, ai, Ri, KOUT, ROUT);                                                           \
+    }
+    CTR_RK4_STAGE(k1, k2, r2, h2)
+    CTR_RK4_STAGE(k2, k3, r3, h2)
+    CTR_RK4_STAGE(k3, k4, r4, h)
+#undef CTR_RK4_STAGE
+    const double h6 = h * (1.0 / 6.0);
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (i < N) {
+            yu[i] = fma(h6, k1.uz[i] + 2.0 * (k2.uz[i] + k3.uz[i]) + k4.uz[i], yu[i]);
+            ya[i] = fma(h6, k1.al[i] + 2.0 * (k2.al[i] + k3.al[i]) + k4.al[i], ya[i]);
+        }
+        yr[i] = fma(h6, r1[i] + 2.0 * (r2[i] + r3[i]) + r4[i], yr[i]);
+    }
+    #pragma unroll
+    for (int i = 0; i < 9; ++i) yR[i] = fma(h6, k1.R[i] + 2.0 * (k2.R[i] + k3.R[i]) + k4.R[i], yR[i]);
+}
+
+// The plan of a fixed-step RK4 FK, computed for every kept gap before any integration (one
+// convergent block instead of a division and a ceil at every segment start, which run under
+// exec masks whenever some lane of the wave starts a segment): step count n_k and size h_k per
+// gap in this lane's LDS columns, the gaps with steps to take, and the gaps integrated in closed
+// form.  Gap k spans [S_k, S_{k+1} - 1e-6] (model.py:141, reversed spans sorted as :145-151) with
+// n = max(1, ceil(len * steps_per_m)) equal steps (oracle rk4_span).  A segment whose RHS has a
+// constant curvature runs as one segment map (rigid_segment_map): every gap of the rigid model,
+// and with the compliant model (no y pre-curvature) the trailing gaps where tube 0 is alone ("Tube
+// levels": u' = 0 there; the present set only shrinks along a backbone, so they come last).  A gap
+// over RK4_MAX_STEPS steps ends the plan there (CTR_STATUS_TOO_LONG, NaN tip), as the oracle stops.
+__shared__ int s_seg_n[9][CTR_BLOCK];
+
+struct Rk4Plan {
+    uint32_t step;     // kept gaps integrated stage by stage, in arclength order
+    uint32_t tail;     // kept gaps after them, each as one segment map
+    bool too_long;
+};
+
+template <bool LEVELS, bool RIGID>
+__device__ __forceinline__ Rk4Plan rk4_plan(const Seg &sg, double *end_lds, int *n_lds, double steps_per_m)
+{
+    Rk4Plan pl = {0u, 0u, false};
+    double prev_end = 0.0;
+    uint32_t live = 0u;                       // gaps with at least one step
+    #pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        if (!((sg.kept >> k) & 1u) || pl.too_long) continue;
+        const double endk = end_lds[k * CTR_BLOCK];
+        const double a = prev_end, b = endk - 1e-6;
+        const double len = fmax(a, b) - fmin(a, b);
+        prev_end = endk;
+        if (!(len > 0.0)) continue;
+        const double nf = ceil(len * steps_per_m);
+        if (!(nf <= (double)RK4_MAX_STEPS)) {  // joints far outside the Box
+            pl.too_long = true;
+            continue;
+        }
+        const int n = max(1, (int)nf);
+        end_lds[k * CTR_BLOCK] = len / n;      // h_k replaces the gap's end (not read again)
+        n_lds[k * CTR_BLOCK] = n;
+        live |= 1u << k;
+    }
+    if (RIGID) {
+        pl.tail = live;
+    } else if (LEVELS) {
+        // tube 0 alone on gap k: present bits (pc bits 9 i + k) = {0}
+        const uint32_t t0 = (uint32_t)(sg.pc & 0x1FFu), t1 = (uint32_t)((sg.pc >> 9) & 0x1FFu),
+                       t2 = (uint32_t)((sg.pc >> 18) & 0x1FFu);
+        const uint32_t notalone = live & ~(t0 & ~t1 & ~t2);
+        const uint32_t upto = notalone ? (2u << (31 - __builtin_clz(notalone))) - 1u : 0u;
+        pl.step = live & upto;
+        pl.tail = live & ~upto;
+    } else {
+        pl.step = live;
+    }
+    return pl;
+}
+
 template <bool HAS_UY, bool RIGID, bool CAREFUL = true>
 __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], FkStats &st, double steps_per_m)
 {
+    constexpr bool LEVELS = !HAS_UY && !RIGID;
     const double beta[3] = {q[0], q[1], q[2]};
     double *end_lds = &s_seg_end[0][threadIdx.x];
+    int *n_lds = &s_seg_n[0][threadIdx.x];
     const Seg sg = seg_build(sy, beta, end_lds);
+    const Rk4Plan pl = rk4_plan<LEVELS, RIGID>(sg, end_lds, n_lds, steps_per_m);
+    st.nseg += (uint32_t)__builtin_popcount(sg.kept);
     double yu[3] = {0.0, 0.0, 0.0};
     double ya[3] = {q[3], q[4], q[5]};
     double yr[3] = {0.0, 0.0, 0.0};
@@ -1238,89 +1358,67 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
         yR[3] = s0; yR[4] = c0;  yR[5] = 0.0;
         yR[6] = 0.0; yR[7] = 0.0; yR[8] = 1.0;
     }
-    const Trig tconst = trig_of<CAREFUL>(ya);     // RIGID: the tube angles never change
-    SegPar p;
-    double h = 0.0, prev_end = 0.0;
-    int left = 0;                        // RK4 steps left in the current segment
-    uint32_t remaining = sg.kept;
-    for (;;) {
-        if (left == 0) {
-            if (remaining == 0) break;
-            const int k = __builtin_ctz(remaining);
-            remaining &= remaining - 1u;
-            p = seg_par_at<HAS_UY, RIGID>(sy, seg_bits(sg, k));
-            const double endk = end_lds[k * CTR_BLOCK];
-            const double a = prev_end, b = endk - 1e-6;
-            const double len = fmax(a, b) - fmin(a, b);
-            prev_end = endk;
-            st.nseg++;
-            const double nf = ceil(len * steps_per_m);
-            if (len > 0.0 && !(nf <= (double)RK4_MAX_STEPS)) {   // joints far outside the Box
-                yr[0] = yr[1] = yr[2] = NAN;
-                st.status |= CTR_STATUS_TOO_LONG | CTR_STATUS_NAN;
-                break;
+    if constexpr (!RIGID) {
+        // stepped gaps: one RK4 step per iteration (lanes in lock-step, each in its own gap); the
+        // step runs at the wave's tube level
+        SegPar p;
+        double h = 0.0;
+        int left = 0;                         // steps left in the current gap
+        bool lv3 = true;
+        uint32_t rem = pl.step;
+        for (;;) {
+            if (left == 0) {
+                if (rem == 0u) break;
+                const int k = __builtin_ctz(rem);
+                rem &= rem - 1u;
+                p = seg_par_at<HAS_UY, false>(sy, seg_bits(sg, k));
+                h = end_lds[k * CTR_BLOCK];
+                left = n_lds[k * CTR_BLOCK];
+                lv3 = (p.present & 4u) != 0u || p.present == 0u;
             }
-            left = (len > 0.0) ? max(1, (int)nf) : 0;
-            h = (left > 0) ? len / left : 0.0;
-            if (RIGID) {
-                // the segment's `left` steps at once: [R | r] M^left (rigid_segment_map)
-                if (left > 0) {
-                    double aq[9], am[3];
-                    st.nrej += (uint32_t)rigid_segment_map<HAS_UY>(p, tconst, yu, h, left, aq, am);   // compositions
-                    double nR[9];
-                    #pragma unroll
-                    for (int r = 0; r < 3; ++r) {
-                        #pragma unroll
-                        for (int c = 0; c < 3; ++c)
-                            nR[3 * r + c] = fma(yR[3 * r + 2], aq[6 + c], fma(yR[3 * r + 1], aq[3 + c], yR[3 * r] * aq[c]));
-                        yr[r] = fma(yR[3 * r + 2], am[2], fma(yR[3 * r + 1], am[1], fma(yR[3 * r], am[0], yr[r])));
-                    }
-                    #pragma unroll
-                    for (int i = 0; i < 9; ++i) yR[i] = nR[i];
-                    st.nfev += 4 * left;
-                    st.nstep += left;
-                    left = 0;
-                }
+            bool lower = false;
+            if constexpr (LEVELS) lower = __ballot(lv3) == 0;
+            if constexpr (LEVELS) {
+                if (lower) rk4_step<2, false, CAREFUL>(p, h, yu, ya, yr, yR);
+                else rk4_step<3, false, CAREFUL>(p, h, yu, ya, yr, yR);
+            } else {
+                rk4_step<3, HAS_UY, CAREFUL>(p, h, yu, ya, yr, yR);
             }
-            continue;
+            st.nfev += 4;
+            st.nstep++;
+            --left;
         }
-        // compliant model: one classical RK4 step of the full nonlinear state (RIGID never gets here)
-        Stage k1, k2, k3, k4;
-        double r1[3], r2[3], r3[3], r4[3];
-        double ui[3], ai[3], Ri[9];
-        {
-            const Trig tt = RIGID ? tconst : trig_of<CAREFUL>(ya);
-            rhs_core<HAS_UY>(p, tt, yu, yR, k1.uz, k1.R);
-            stage_at(p, tt, yu, yR, k1, r1);
+    }
+    // closed-form gaps (every lane of the wave together): [R | r] M^n per gap (rigid_segment_map).
+    // Rigid: the tube angles keep their joint values.  Compliant level 1: u = (u_x,0, 0, u_z,0) is
+    // constant (wx_1 = wx_2 = 0 make the trig irrelevant); alpha is not advanced, nothing reads it.
+    const Trig tc = RIGID ? trig_of<CAREFUL>(ya) : Trig{0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    uint32_t tail = pl.tail;
+    while (__ballot(tail != 0u) != 0) {
+        if (tail != 0u) {
+            const int k = __builtin_ctz(tail);
+            tail &= tail - 1u;
+            const SegPar p = seg_par_at<HAS_UY, RIGID>(sy, seg_bits(sg, k));
+            const int n = n_lds[k * CTR_BLOCK];
+            double aq[9], am[3];
+            const int ncomp = rigid_segment_map<HAS_UY>(p, tc, yu, end_lds[k * CTR_BLOCK], n, aq, am);
+            double nR[9];
+            #pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                #pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    nR[3 * r + c] = fma(yR[3 * r + 2], aq[6 + c], fma(yR[3 * r + 1], aq[3 + c], yR[3 * r] * aq[c]));
+                yr[r] = fma(yR[3 * r + 2], am[2], fma(yR[3 * r + 1], am[1], fma(yR[3 * r], am[0], yr[r])));
+            }
+            #pragma unroll
+            for (int i = 0; i < 9; ++i) yR[i] = nR[i];
+            st.nfev += 4u * (uint32_t)n;      // the RK4 steps the map stands for (oracle nfev)
+            st.nrej += (1u << 16) + (uint32_t)ncomp;   // one segment map + its compositions
         }
-        const double h2 = 0.5 * h;
-#define CTR_RK4_STAGE(KIN, KOUT, ROUT, C)                                                      \
-        {                                                                                      \
-            _Pragma("unroll") for (int i = 0; i < 3; ++i) {                                    \
-                ui[i] = fma(KIN.uz[i], C, yu[i]);                                              \
-                ai[i] = fma(KIN.al[i], C, ya[i]);                                              \
-            }                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < 9; ++i) Ri[i] = fma(KIN.R[i], C, yR[i]);     \
-            const Trig tt = RIGID ? tconst : trig_of<CAREFUL>(ai);                                \
-            rhs_core<HAS_UY>(p, tt, ui, Ri, KOUT.uz, KOUT.R);                                  \
-            stage_at(p, tt, ui, Ri, KOUT, ROUT);                                               \
-        }
-        CTR_RK4_STAGE(k1, k2, r2, h2)
-        CTR_RK4_STAGE(k2, k3, r3, h2)
-        CTR_RK4_STAGE(k3, k4, r4, h)
-#undef CTR_RK4_STAGE
-        const double h6 = h * (1.0 / 6.0);
-        #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            yu[i] = fma(h6, k1.uz[i] + 2.0 * (k2.uz[i] + k3.uz[i]) + k4.uz[i], yu[i]);
-            ya[i] = fma(h6, k1.al[i] + 2.0 * (k2.al[i] + k3.al[i]) + k4.al[i], ya[i]);
-            yr[i] = fma(h6, r1[i] + 2.0 * (r2[i] + r3[i]) + r4[i], yr[i]);
-        }
-        #pragma unroll
-        for (int i = 0; i < 9; ++i) yR[i] = fma(h6, k1.R[i] + 2.0 * (k2.R[i] + k3.R[i]) + k4.R[i], yR[i]);
-        st.nfev += 4;
-        st.nstep++;
-        --left;
+    }
+    if (pl.too_long) {
+        yr[0] = yr[1] = yr[2] = NAN;
+        st.status |= CTR_STATUS_TOO_LONG | CTR_STATUS_NAN;
     }
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;

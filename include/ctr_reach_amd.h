@@ -328,9 +328,12 @@ const char *ctr_last_error(void);
 
 /* Batched Model.forward_kinematics: joints [n][6] f32 -> tip [n][3] f64.
  * sys_idx: [n] or NULL (all system 0).  stats: [n][4] or NULL = {RHS evaluations, accepted
- * RK steps, rejected RK attempts, integrated segments}; fixed-step RK4 never rejects, and with
- * the rigid model stats[2] counts the map compositions of the segments' matrix powers
- * (the executed work of that path).  status: [n] or NULL.  (device) */
+ * RK steps, rejected RK attempts, integrated segments}.  Fixed-step RK4 never rejects; there
+ * stats[1] counts the steps taken stage by stage and stats[2] the executed work of the segments
+ * run as segment maps (matrix powers: every segment of the rigid model, the trailing segments of
+ * the compliant model where tube 0 is alone): maps << 16 | square-and-multiply compositions.
+ * stats[0] counts 4 RHS per RK4 step, mapped or not (the oracle's count).  status: [n] or NULL.
+ * (device) */
 int ctr_fk(const float *joints, const int32_t *sys_idx, int64_t n, const ctr_env_config_t *cfg,
            double *tip, uint32_t *stats, uint32_t *status, void *stream);
 

@@ -5,7 +5,8 @@ Writes:
   profiles/<tag>_pmc.json           per-kernel PMC averages (per launch)
   profiles/<tag>_traffic_calibration.json  FETCH_SIZE / WRITE_SIZE against known byte counts in
                                     k_step's access shapes (tools/traffic_probe.hip)
-  profiles/traffic.json             HBM bytes per k_step launch for bench.py's roofline.traffic:
+  profiles/traffic.json             (traffic_c<config>.json for another bench config, argv[2])
+                                    HBM bytes per k_step launch for bench.py's roofline.traffic:
                                     FETCH_SIZE and WRITE_SIZE scaled by the calibrated factors
                                     (KiB -> bytes)
 """
@@ -19,6 +20,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+# the bench config the passes ran (bench.py --config, from BENCH_ARGS): 3 (the headline) writes
+# profiles/traffic.json, another config profiles/traffic_c<config>.json
+config = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -81,7 +85,7 @@ if step:
     envs = 65536
     rf = cal["read_factor_rows_warm"] if cal else 2.0
     wf = cal["write_factor_rows"] if cal else 1.0
-    t = {"envs": envs, "kernel": step[0], "fetch_size_bytes_raw": fetch, "write_size_bytes_raw": write,
+    t = {"envs": envs, "config": config, "kernel": step[0], "fetch_size_bytes_raw": fetch, "write_size_bytes_raw": write,
          "read_factor": rf, "write_factor": wf,
          "bytes_per_launch": rf * fetch + wf * write,
          "read_bytes": rf * fetch, "write_bytes": wf * write,
@@ -99,7 +103,7 @@ if step:
         if len(dur) >= 32:
             t["avg_ns_rocprof_bench_timed_32"] = sum(dur[-32:]) / 32.0
             t["launches_in_trace"] = len(dur)
-    with open(os.path.join(dst, "traffic.json"), "w") as fh:
+    with open(os.path.join(dst, "traffic.json" if config == 3 else "traffic_c%d.json" % config), "w") as fh:
         json.dump(t, fh, indent=1)
     print(json.dumps(t, indent=1))
 for k, v in avg_ns.items():
