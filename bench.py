@@ -317,10 +317,29 @@ def cpu_baseline(args, cfgd):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
-    return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "%d envs x %d steps (%d auto-resets, staggered episode clocks) of oracle/ctr_oracle.c "
-                      "(%s, %s model, fp64), OpenMP %d threads, %.1f s" % (n, steps, resets, cfgd["integrator"],
-                                                                           cfgd["model"], threads, el)}
+    out = {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "sample": "%d envs x %d steps (%d auto-resets, staggered episode clocks) of oracle/ctr_oracle.c "
+                     "(%s, %s model, fp64), OpenMP %d threads, %.1f s" % (n, steps, resets, cfgd["integrator"],
+                                                                          cfgd["model"], threads, el)}
+    # the reference's own CPU path (scipy solve_ivp, pure Python) cannot travel to this host: its
+    # figures were measured in the build container (tools/time_reference.py), together with the
+    # same port on the same cores, which calibrates the port against the reference per core
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_reference_r01.json")) as fh:
+            ref = json.load(fh)
+        per_core = ref["port_over_reference_1core"]
+        out["reference_python_here"] = {
+            "env_steps_per_s_1core": ref["env_steps_per_s_1proc"],
+            "env_steps_per_s_%dcores" % ref["nproc"]: ref["env_steps_per_s_nproc"],
+            "what": ref["what"], "cpu": ref["cpu"] + " (the build container, not this host)",
+            "port_over_reference_per_core": per_core,
+            "reference_equivalent_on_these_cores": (out["value"] / per_core
+                                                    if cfgd["integrator"] == "rk45_scipy" else None),
+            "source": "profiles/cpu_reference_r01.json (tools/time_reference.py: CtrReachEnv.step() of the unmodified "
+                      "reference, default kwargs, 20 s per run)"}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def main():
@@ -542,6 +561,21 @@ def main():
         resets = int(rt.item())
     total_steps = n * ws * args.steps
 
+    # ---- k_step as the window runs it (pooled auto-resets), from the window's end state (right
+    # after a refill): R - 1 back-to-back step launches bracketed by one event pair on the launch
+    # stream, no refill among them (the R-th step, untimed, brings the refill that falls due).
+    # Without the per-step gather only (its steps also wait for / launch the gather).
+    k_ms_pooled = None
+    if not gather and R_steps > 1 and env._steps_since_refill == 0:
+        ep0, ep1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ep0.record(stream)
+        for i in range(R_steps - 1):
+            one_step(i)
+        ep1.record(stream)
+        one_step(R_steps - 1)
+        torch.cuda.synchronize()
+        k_ms_pooled = ep0.elapsed_time(ep1) / (R_steps - 1)
+
     # ---- dominant kernel (k_step) alone: HIP events on the launch stream, no auto-reset.
     # ctr_step with autoreset = 0 launches exactly one kernel (k_step) on `stream`; one event pair
     # brackets k_iters back-to-back launches (per-launch event pairs add their own few us), so the
@@ -624,6 +658,15 @@ def main():
                      "frac": achieved_tf / PEAK_FP64_VALU, "traffic": traffic,
                      "traffic_source": traffic_note,
                      "kernel": "k_step", "kernel_ms": k_ms,
+                     "kernel_autoreset": "off (achieved / frac time k_step with CTR_AUTORESET_OFF: 32 back-to-back "
+                                         "launches from the window's joints, the FK work priced on those joints)",
+                     "kernel_ms_autoreset_pooled": k_ms_pooled,
+                     "frac_autoreset_pooled": (flops_env_step / (k_ms_pooled * 1e-3) / 1e12 / PEAK_FP64_VALU
+                                               if k_ms_pooled else None),
+                     "kernel_ms_autoreset_pooled_note": ("k_step as the window launches it (CTR_AUTORESET_POOLED: done "
+                                                         "envs copy their precomputed reset), %d back-to-back launches "
+                                                         "after the window, no refill among them; its frac prices the "
+                                                         "same FK work as kernel_ms" % (R_steps - 1)),
                      "flops_per_launch": flops_env_step, "sincos_per_launch": sincos,
                      "nfev_per_env_step": nfev_mean,
                      "bytes_per_launch_algorithmic": BYTES_STEP * n,

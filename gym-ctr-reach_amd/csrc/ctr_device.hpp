@@ -702,13 +702,6 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
                         const FkSuspend *from = nullptr, FkSuspend *to = nullptr, int budget = 0)
 {
     using namespace rk;
-#if defined(CTR_DIAG_NOFK)
-    // timing diagnostic only (tools/experiments): the FK skipped, so a launch times the rest
-    if constexpr (!RESUME && !SHAPE) {
-        tip[0] = q[0]; tip[1] = q[1]; tip[2] = q[2];
-        return true;
-    }
-#endif
     // f's alpha part is the masked u_z of y (stage_at, and K6 -> f on acceptance): it is read
     // from y instead of being carried in f (three fewer loop-carried doubles)
 #define CTR_FAL(i) ((i) == 0 ? (((p.present & 1u) != 0u) ? yu[0] : 0.0) : yu[i])

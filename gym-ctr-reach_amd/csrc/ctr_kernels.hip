@@ -739,19 +739,6 @@ __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batc
 // SEG_GROUP lanes, whose segments run in parallel (fk_group_rigid4); other modes: one env per lane.
 // HER: record the step into the HER store (ctr_step_her); a compile-time switch, so the plain
 // step carries no trace of it (a runtime flag measured +2.3 us on k_step).
-#if defined(CTR_DIAG_WAVETIME)
-// timing diagnostic only (tools/wave_times.py): per wave, on the 100 MHz clock, the kernel's start,
-// the FK's start and end (lane 0's env), the finish's end, the appends' end and the kernel's end
-__device__ unsigned long long g_diag_wave_t[8192][6];
-#define CTR_DIAG_STAMP(k)                                                                        \
-    do {                                                                                         \
-        if ((threadIdx.x & 63) == 0)                                                             \
-            g_diag_wave_t[blockIdx.x * (BLOCK / 64) + threadIdx.x / 64][k] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#else
-#define CTR_DIAG_STAMP(k)
-#endif
-
 template <int MODE, bool HER>
 __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, const float *__restrict__ actions,
                                           const ctr_step_out_t &o, int32_t autoreset, const HerK &hk)
@@ -849,15 +836,12 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         set_action_substeps(sy, kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);
         FkStats st = {0, 0, 0, 0, 0};
         double ag[3];
-        CTR_DIAG_STAMP(1);
         fk_dispatch<MODE>(kc, episode_sys(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e)), q, ag, st);
-        CTR_DIAG_STAMP(2);
         double dg_f[3];
         #pragma unroll
         for (int i = 0; i < 3; ++i) dg_f[i] = s_fin_dg[i][threadIdx.x];
         step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, s_fin_t[threadIdx.x],
                     s_fin_ep[threadIdx.x], dg_f, grow);
-        CTR_DIAG_STAMP(3);
     }
     if (autoreset) {
         if (autoreset == CTR_AUTORESET_POOLED) {
@@ -873,7 +857,6 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
             wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
         }
     }
-    CTR_DIAG_STAMP(4);
     if (gp) {
         // the fused push (every lane of the wave here): once every consumer has released the
         // slot (normally known since the staging), each env's row into every rank's ring with
@@ -892,17 +875,7 @@ template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
                                                    ctr_step_out_t o, int32_t autoreset)
 {
-#if defined(CTR_DIAG_WAVETIME)
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#endif
     step_body<MODE, false>(kc, b, actions, o, autoreset, HerK{});
-#if defined(CTR_DIAG_WAVETIME)
-    const int w = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);
-    if ((threadIdx.x & 63) == 0 && w < 8192) {
-        g_diag_wave_t[w][0] = t0;
-        g_diag_wave_t[w][5] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
 
 template <int MODE>
@@ -1653,16 +1626,6 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
 }
 
 }  // namespace
-
-#if defined(CTR_DIAG_WAVETIME)
-extern "C" int ctr_diag_wavetimes(unsigned long long *dst, int n)
-{
-    if (!dst || n < 0 || n > 8192) return fail(CTR_EINVAL, "ctr_diag_wavetimes: bad arguments");
-    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_diag_wave_t), (size_t)n * 48, 0, hipMemcpyDeviceToHost) != hipSuccess)
-        return hip_check("ctr_diag_wavetimes");
-    return 0;
-}
-#endif
 
 extern "C" {
 

@@ -5,8 +5,8 @@ end, and the kernel's end on the
 Is the launch as long as its slowest wave with the others close behind (per-iteration cost is the
 lever), or do a few waves trail the rest (work balance is)?
 
-build: make -C gym-ctr-reach_amd HIPFLAGS="<the Makefile's flags> -DCTR_DIAG_WAVETIME" \\
-           LIB=ctr_reach_amd/lib/libab_wavet.so ctr_reach_amd/lib/libab_wavet.so
+build: PATCH=tools/experiments/diag.patch EXTRA=-DCTR_DIAG_WAVETIME bash tools/experiments/build_rev.sh HEAD wavet
+       (the diagnostic is a patch, not part of the product sources)
 usage: CTR_REACH_AMD_LIB=.../libab_wavet.so python tools/wave_times.py [n_envs]"""
 import ctypes
 import os
