@@ -245,7 +245,9 @@ __device__ __forceinline__ void gather_store_row(const ctr_gather_push_t *g, int
     const int W = g->world;
     for (int k = 0; k < W; ++k) {
         row16_t *dst = static_cast<row16_t *>(g->dst[k]) + e;
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(dst), "v"(v) : "memory");
+        // the s_nop inside the statement: a VALU write of a > 8-byte store's data VGPRs needs wait
+        // states after the store, and the compiler's hazard recognizer cannot see into the asm
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
     }
 }
 
@@ -291,14 +293,34 @@ __device__ __forceinline__ bool gather_slot_free(const ctr_gather_push_t *g, uin
     return __ballot(!seq_reached(rel, seq - (uint32_t)g->depth)) == 0;
 }
 
-// Bounded wait (every lane active) for the slot of step seq; false after spin_limit polls.
+// Bounded waits have a wall-clock budget: s_memrealtime counts at 100 MHz.
+__device__ __forceinline__ bool wait_expired(uint64_t t0, uint32_t wait_us)
+{
+    return __builtin_amdgcn_s_memrealtime() - t0 >= (uint64_t)wait_us * 100u;
+}
+
+// Bounded wait (every lane active) for the slot of step seq; false after wait_us microseconds.
 __device__ __noinline__ bool gather_wait_slot(const ctr_gather_push_t *g, uint32_t seq)
 {
-    for (uint32_t k = 0;; ++k) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
         if (gather_slot_free(g, seq, gather_release_load(g, seq))) return true;
-        if (k >= g->spin_limit) return false;
+        if (wait_expired(t0, g->wait_us)) return false;
         __builtin_amdgcn_s_sleep(8);
     }
+}
+
+// The release wait of step seq timed out: lane c < world whose consumer c has not released the
+// slot stores seq into this rank's poison word in c's memory (system scope), and the wave waits
+// for those stores before any of its rows overwrite the slot -- so a consumer that reads its
+// poison words after reading a view sees every overwrite that reached it (include/ctr_reach_amd.h).
+__device__ __noinline__ void gather_poison_lanes(const ctr_gather_push_t *g, uint32_t seq)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    if (lane < g->world && !seq_reached(__hip_atomic_load(g->rel + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                                        seq - (uint32_t)g->depth))
+        __hip_atomic_store(g->poisonw[lane], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // The fused consumer wait (ctr_step_out_t.gather_wait_prev): lane k < world polls this rank's
@@ -309,13 +331,18 @@ __device__ __noinline__ void gather_wait_prev_lane(const ctr_gather_push_t *g, u
 {
     const int lane = (int)threadIdx.x;
     if (lane >= g->world) return;
-    for (uint32_t k = 0;; ++k) {
+    // producer `lane` overran a slot of this rank before (its poison word): the views this rank
+    // read before this launch may hold rows of a later step
+    if (__hip_atomic_load(g->poison + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+        atomicOr(g->err, CTR_GATHER_E_RELEASE_TIMEOUT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
         const uint32_t v = __hip_atomic_load(g->wait_seqw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (seq_reached(v, seq)) {
             if (v != seq) atomicOr(g->err, CTR_GATHER_E_OVERWRITTEN);
             return;
         }
-        if (k >= g->spin_limit) {
+        if (wait_expired(t0, g->wait_us)) {
             atomicOr(g->err, CTR_GATHER_E_PREV_TIMEOUT);
             return;
         }
@@ -862,8 +889,10 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         // slot (normally known since the staging), each env's row into every rank's ring with
         // system-scope stores, waited on, so the rows are performed at system scope before the
         // wave ends and the next launch publishes the sequence words (include/ctr_reach_amd.h)
-        if (!slot_free0 && !gather_wait_slot(gp, o.gather_seq) && (threadIdx.x & 63) == 0)
-            atomicOr(gp->err, CTR_GATHER_E_RELEASE_TIMEOUT);
+        if (!slot_free0 && !gather_wait_slot(gp, o.gather_seq)) {
+            if ((threadIdx.x & 63) == 0) atomicOr(gp->err, CTR_GATHER_E_RELEASE_TIMEOUT);
+            gather_poison_lanes(gp, o.gather_seq);       // the overrun consumers learn it too
+        }
         if (live) gather_store_row(gp, e, grow);
         gather_rows_performed();
         if (o.gather_wait_prev && blockIdx.x == 0 && threadIdx.x < 64)

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 13
+CTR_ABI_VERSION = 14
 CTR_IPC_HANDLE_BYTES = 64
 CTR_GATHER_MAX_RANKS = 16
 CTR_MAX_SYSTEMS = 8
@@ -124,9 +124,10 @@ class CtrStepOut(ctypes.Structure):
 class CtrGatherPush(ctypes.Structure):
     _fields_ = [("src", _P), ("n", ctypes.c_int64), ("world", ctypes.c_int32), ("pad", ctypes.c_int32),
                 ("dst", _P * CTR_GATHER_MAX_RANKS), ("seqw", _P * CTR_GATHER_MAX_RANKS), ("ticket", _P),
-                # fused push flow control (ABI 13)
+                # fused push flow control (ABI 13; wait_us a wall-clock budget and the poison words: ABI 14)
                 ("relw", _P * CTR_GATHER_MAX_RANKS), ("rel", _P), ("wait_seqw", _P), ("err", _P),
-                ("depth", ctypes.c_int32), ("spin_limit", ctypes.c_uint32)]
+                ("depth", ctypes.c_int32), ("wait_us", ctypes.c_uint32),
+                ("poisonw", _P * CTR_GATHER_MAX_RANKS), ("poison", _P)]
 
 
 CTR_GATHER_E_WAIT_TIMEOUT = 1       # a consumer wait gave up

@@ -170,7 +170,8 @@ class HipCopyOps(object):
         """Per-slot ctr_gather_push_t descriptors in device memory (the fused push reads them):
         targets[slot] = [(row block dst, sequence word), ...] per rank; flow = the flow-control
         fields (relw: this rank's release word in every rank, rel, wait_seqw per slot, err, depth,
-        spin_limit).  Returns (keep-alive, device pointer per slot)."""
+        wait_us, poisonw: this rank's poison word in every rank, poison).  Returns (keep-alive,
+        device pointer per slot)."""
         import ctypes
         import torch
         size = ctypes.sizeof(self._abi.CtrGatherPush)
@@ -183,7 +184,10 @@ class HipCopyOps(object):
             for k, rw in enumerate(flow["relw"]):
                 g.relw[k] = rw
             g.rel, g.wait_seqw, g.err = flow["rel"], flow["wait_seqw"][slot], flow["err"]
-            g.depth, g.spin_limit = flow["depth"], flow["spin_limit"]
+            g.depth, g.wait_us = flow["depth"], flow["wait_us"]
+            for k, pw in enumerate(flow["poisonw"]):
+                g.poisonw[k] = pw
+            g.poison = flow["poison"]
             raw += bytes(g)
         dev = torch.frombuffer(raw, dtype=torch.uint8).to(self.device)
         return dev, [dev.data_ptr() + i * size for i in range(len(targets))]
@@ -209,8 +213,8 @@ class HipCopyOps(object):
         rc = self.lib.ctr_copy_list(arr, n, sp, len(streams), ready_event.cuda_event if ready_event else None, dp)
         self._abi.check(rc, "ctr_copy_list")
 
-    def wait(self, seqw_ptr, n, seq, spin_limit, err, stream):
-        rc = self.lib.ctr_gather_wait(seqw_ptr, n, seq & 0xFFFFFFFF, spin_limit, err.data_ptr(), stream.cuda_stream)
+    def wait(self, seqw_ptr, n, seq, wait_us, err, stream):
+        rc = self.lib.ctr_gather_wait(seqw_ptr, n, seq & 0xFFFFFFFF, wait_us, err.data_ptr(), stream.cuda_stream)
         self._abi.check(rc, "ctr_gather_wait")
 
     def view(self, ptr, shape, dtype):
@@ -262,7 +266,7 @@ class PushGather(object):
     ``ops`` is the device backend (HipCopyOps; tests pass a CPU stand-in)."""
 
     def __init__(self, n, group=None, depth=3, engine="fused", n_streams=None, device=None, ops=None,
-                 spin_limit=1 << 22, wait_prev=False):
+                 wait_us=10_000_000, wait_prev=False):
         import torch
         import torch.distributed as dist
         if engine not in ("fused", "sdma"):
@@ -278,17 +282,20 @@ class PushGather(object):
             raise ValueError("at most 16 ranks (CTR_GATHER_MAX_RANKS)")
         self.wait_prev = bool(wait_prev)
         self.ops = ops if ops is not None else HipCopyOps(device)
-        self.spin_limit = int(spin_limit)
+        if not 0 < int(wait_us) < 1 << 32:
+            raise ValueError("wait_us must fit a uint32 (microseconds)")
+        self.wait_us = int(wait_us)
         W, n4 = self.world, self.n * PACK_WIDTH * 4
         self.block_bytes = n4
         self.rel_off = self.depth * W * 4                 # release words, then the push ticket
         ticket_off = self.rel_off + W * 4
+        self.poison_off = ticket_off + 64                 # poison words, after the ticket
         # every rank takes part in both exchanges even after a local failure, and all raise
         # together: a rank that gave up alone would leave the others blocked in a collective
         mine, err = None, None
         try:
             self.recv_ptr = self.ops.alloc_shared(self.depth * W * n4)
-            self.seqw_ptr = self.ops.alloc_shared(ticket_off + 64)
+            self.seqw_ptr = self.ops.alloc_shared(self.poison_off + W * 4)
             mine = (self.ops.handle(self.recv_ptr), self.ops.handle(self.seqw_ptr))
         except Exception as ex:            # noqa: BLE001 -- re-raised below, on every rank
             err = "rank %d: %s" % (self.rank, ex)
@@ -313,13 +320,16 @@ class PushGather(object):
         self.recv = self.ops.view(self.recv_ptr, (self.depth, W, self.n, PACK_WIDTH), torch.float32)
         self.seqw = self.ops.view(self.seqw_ptr, (self.depth, W), torch.int32)
         self.rel = self.ops.view(self.seqw_ptr + self.rel_off, (W,), torch.int32)
+        self.poison = self.ops.view(self.seqw_ptr + self.poison_off, (W,), torch.int32)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.pending = 0          # fused: the last pushed step whose words are not yet published
         if engine == "fused":
             flow = {"relw": [self.peer_seqw[p] + self.rel_off + 4 * self.rank for p in range(W)],
                     "rel": self.seqw_ptr + self.rel_off,
                     "wait_seqw": [self.seqw_ptr + ((s - 1) % self.depth) * W * 4 for s in range(self.depth)],
-                    "err": self.err.data_ptr(), "depth": self.depth, "spin_limit": self.spin_limit}
+                    "err": self.err.data_ptr(), "depth": self.depth, "wait_us": self.wait_us,
+                    "poisonw": [self.peer_seqw[p] + self.poison_off + 4 * self.rank for p in range(W)],
+                    "poison": self.seqw_ptr + self.poison_off}
             self._desc_keep, self.desc = self.ops.upload_descriptors(
                 [self.targets(s) for s in range(self.depth)], self.n, self.ticket_ptr, flow)
             self.n_streams = 0
@@ -380,8 +390,21 @@ class PushGather(object):
         if self.engine == "fused" and self.pending == seq:
             self.ops.publish(self.desc[slot], seq, stream)     # no later step has published it
             self.pending = 0
-        self.ops.wait(self.seqw_ptr + slot * self.world * 4, self.world, seq, self.spin_limit, self.err, stream)
+        self.ops.wait(self.seqw_ptr + slot * self.world * 4, self.world, seq, self.wait_us, self.err, stream)
         return self.slot_view(seq)
+
+    def err_bits(self):
+        """This rank's CTR_GATHER_E_* bits, with a producer's overrun of a slot this rank had not
+        released (its poison word, fused engine) as CTR_GATHER_E_RELEASE_TIMEOUT.  Synchronises.
+        Read after a view's readers have run, it covers every overwrite that reached that view
+        (the producer's poison store is performed before its first row store)."""
+        import torch
+        if torch.is_tensor(self.err) and self.err.is_cuda:
+            torch.cuda.synchronize(self.err.device)
+        e = int(self.err.reshape(-1)[0].item()) & 0xFFFFFFFF
+        if self.engine == "fused" and bool((self.poison != 0).any()):
+            e |= 4                                           # CTR_GATHER_E_RELEASE_TIMEOUT
+        return e
 
     def flush(self, stream):
         """Publish the last pushed step's sequence words now (fused engine: a step's words are
@@ -419,7 +442,8 @@ def verify_gathered(out, mine, err, group=None):
     ref = torch.cat(blocks)
     got = out.cpu() if gloo else out
     bad_rows = int((got != ref).any(dim=1).sum().item())
-    e = int(err.item()) if hasattr(err, "item") else int(err)
+    # err: the error word, or a callable returning the bits (PushGather.err_bits), read after the rows
+    e = err() if callable(err) else (int(err.item()) if hasattr(err, "item") else int(err))
     flags = torch.tensor([1 if bad_rows else 0, e, bad_rows], dtype=torch.int64,
                          device="cpu" if gloo else out.device)
     dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
@@ -437,7 +461,7 @@ def check_push_steps(step, gather, mine, steps, stream=None, group=None):
     rep = {"steps_checked": 0}
     for i in range(steps):
         seq = step(i)
-        ok, r = verify_gathered(gather.wait(seq, stream), mine(), gather.err, group=group)
+        ok, r = verify_gathered(gather.wait(seq, stream), mine(), gather.err_bits, group=group)
         rep["steps_checked"] += 1
         if not ok:
             rep.update(r, failed_at_step=i)

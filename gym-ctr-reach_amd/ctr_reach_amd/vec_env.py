@@ -526,16 +526,20 @@ class CtrReachVecEnv(object):
         out["table"] = table
         return out
 
-    def enable_gather(self, backend="push", group=None, depth=3, wait_prev=False, spin_limit=1 << 22):
+    def enable_gather(self, backend="push", group=None, depth=3, wait_prev=False, wait_us=10_000_000):
         """Set up the push all-gather (collective: every rank calls it).  "push": every later
         step also stores its packed rows into every rank's receive ring (the fused push; no
         extra launch), paced by the ranks' slot releases: the gathered view of step s stays valid
         until this env launches step s + depth - 1; with ``wait_prev`` every step also waits until
         the previous step's rows of every rank are in this rank's ring (depth >= 3).  "sdma":
         gather_outputs(backend="sdma") copies them with the copy engines (needs
-        pack_outputs=True; the caller paces the ranks).  ``spin_limit`` bounds every device-side
-        wait (~0.2-1 us per poll); a wait that gives up sets a CTR_GATHER_E_* bit in the gather's
-        error word instead of hanging.  Returns the distributed.PushGather."""
+        pack_outputs=True; the caller paces the ranks).  ``wait_us`` is the wall-clock budget of every
+        device-side wait, in microseconds (default 10 s: a rank may pause that long between steps
+        -- checkpointing, evaluation -- before its peers' waits give up; raise it for longer
+        pauses); a wait that gives up sets a CTR_GATHER_E_* bit in the gather's error word instead
+        of hanging.  A producer that overruns a slot this rank has not released also flags it here
+        (poison words): ``err_bits()`` read after a view's readers have run covers that view.
+        Returns the distributed.PushGather."""
         if self._push_gather is not None:
             raise RuntimeError("the gather is already enabled")
         if backend == "sdma" and self.packed_bufs is None:
@@ -544,7 +548,7 @@ class CtrReachVecEnv(object):
             raise ValueError("backend must be 'push' or 'sdma'")
         self._push_gather = D.PushGather(self.num_envs, group=group, depth=depth, device=self.device,
                                          engine="fused" if backend == "push" else "sdma",
-                                         wait_prev=wait_prev and backend == "push", spin_limit=spin_limit)
+                                         wait_prev=wait_prev and backend == "push", wait_us=wait_us)
         return self._push_gather
 
     def gather_outputs(self, group=None, async_op=False, backend="rccl", depth=3):

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 13
+#define CTR_ABI_VERSION 14
 #define CTR_MAX_SYSTEMS 8
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
@@ -431,13 +431,22 @@ int ctr_domain_params(const ctr_env_config_t *cfg, const ctr_batch_t *batch, ctr
  * step t - depth (a bounded wait; on time-out the rows are stored anyway and err gets
  * CTR_GATHER_E_RELEASE_TIMEOUT).  ctr_gather_push and ctr_copy_list do not take part in the
  * flow control: their callers pace the ranks.
+ * A time-out is also reported to the consumer it overran (ABI 14): before storing any row, the
+ * producer stores the step into its poison word in the memory of every consumer that had not
+ * released the slot (system scope, waited for), and every k_step with gather_wait_prev folds the
+ * consumer's own poison words into its err (CTR_GATHER_E_RELEASE_TIMEOUT).  So err, read after a
+ * view's readers have run (the next fused step, or PushGather.err_bits()), covers every overwrite
+ * that reached the view -- no cross-rank reduction is needed to trust a local view.
+ * Every bounded wait has a wall-clock budget (wait_us, s_memrealtime at 100 MHz), not a poll count.
  * ------------------------------------------------------------------------------------- */
 #define CTR_IPC_HANDLE_BYTES 64
 #define CTR_GATHER_MAX_RANKS 16
 /* err bits of ctr_gather_wait and of the fused push (ctr_gather_push_t.err) */
-#define CTR_GATHER_E_WAIT_TIMEOUT    1u   /* a consumer wait gave up after spin_limit polls      */
+#define CTR_GATHER_E_WAIT_TIMEOUT    1u   /* a consumer wait gave up after wait_us microseconds  */
 #define CTR_GATHER_E_OVERWRITTEN     2u   /* a sequence word was already past the awaited step   */
-#define CTR_GATHER_E_RELEASE_TIMEOUT 4u   /* a fused push stored into a slot not yet released    */
+#define CTR_GATHER_E_RELEASE_TIMEOUT 4u   /* a fused push stored into a slot not yet released
+                                              (in the producer's err, and via the poison words in
+                                              the err of the consumer it overran)                */
 #define CTR_GATHER_E_PREV_TIMEOUT    8u   /* the fused consumer wait (gather_wait_prev) gave up  */
 
 /* One rank's push of its block: the host struct of ctr_gather_push, and (in device memory) the
@@ -460,7 +469,15 @@ struct ctr_gather_push_t {
                                                  previous slot (gather_wait_prev)           */
     uint32_t   *err;                          /* device word: CTR_GATHER_E_* bits             */
     int32_t     depth;                        /* ring slots (>= 2)                            */
-    uint32_t    spin_limit;                   /* polls before a wait gives up (~0.2 us each)  */
+    uint32_t    wait_us;                      /* wall-clock budget of every bounded wait, in
+                                                 microseconds (ABI 14; was a poll count)     */
+    /* ABI 14: */
+    uint32_t   *poisonw[CTR_GATHER_MAX_RANKS];/* this rank's poison word in rank p's memory: on a
+                                                 release time-out, step seq is stored into the
+                                                 words of the consumers that had not released */
+    const uint32_t *poison;                   /* [world] this rank's poison words (producer p's
+                                                 at [p]; zeroed, sticky): non-zero = a producer
+                                                 overwrote a slot this rank had not released  */
 };
 
 /* Enqueue the push kernel: the n rows to every dst[p] (p < world), then seq to every seqw[p]
@@ -503,10 +520,10 @@ int ctr_copy_list(const ctr_copy_t *copies, int32_t n_copies, void *const *strea
 
 /* Consumer side: enqueue on `stream` a one-wave kernel that waits until seqw[i] reaches seq for
  * every i < n (wrap-aware uint32 compare; seqw is uncached, polled at system scope), then
- * returns.  err (device, uint32) gets bit 1 if spin_limit polls pass first (the kernel then
+ * returns.  err (device, uint32) gets bit 1 if wait_us microseconds pass first (the kernel then
  * returns anyway: no unbounded wait) and bit 2 if a word is already past seq (the slot was
  * overwritten by a later step before it was consumed). */
-int ctr_gather_wait(const uint32_t *seqw, int32_t n, uint32_t seq, uint32_t spin_limit, uint32_t *err,
+int ctr_gather_wait(const uint32_t *seqw, int32_t n, uint32_t seq, uint32_t wait_us, uint32_t *err,
                     void *stream);
 
 /* Batched compute_reward over leading dims: ag, dg [n][3] f64 -> reward [n] f32 in {-1, 0}. */

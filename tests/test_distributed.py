@@ -216,25 +216,35 @@ class _ShmCopyOps(object):
         def reached(a, b):
             return ((a - b) & 0xFFFFFFFF) < 0x80000000
 
-        for k in range(cur["spin_limit"] + 1):
+        deadline = time.monotonic() + cur["wait_us"] * 1e-6     # wall-clock budget (ABI 14)
+        while True:
             if all(reached(r, (seq - cur["depth"]) & 0xFFFFFFFF) for r in rel):
                 break
+            if time.monotonic() >= deadline:
+                err.value |= 4                               # CTR_GATHER_E_RELEASE_TIMEOUT
+                # poison words: every consumer that had not released learns of the overrun
+                for c in range(W):
+                    if not reached(rel[c], (seq - cur["depth"]) & 0xFFFFFFFF):
+                        u32.from_address(cur["poisonw"][c]).value = seq & 0xFFFFFFFF
+                break
             time.sleep(0.0005)
-        else:
-            err.value |= 4                                   # CTR_GATHER_E_RELEASE_TIMEOUT
         for dst, sw in cur["targets"]:
             ctypes.memmove(dst, rows.data_ptr(), rows.numel() * 4)
         if wait_prev:
+            if any(p != 0 for p in (u32 * W).from_address(cur["poison"])):
+                err.value |= 4                               # overrun by a producer (poison word)
             words = (u32 * W).from_address(cur["wait_seqw"])
             want = (seq - 1) & 0xFFFFFFFF
-            for k in range(cur["spin_limit"] + 1):
+            deadline = time.monotonic() + cur["wait_us"] * 1e-6
+            while True:
                 if all(reached(w, want) for w in words):
                     if any(w != want for w in words):
                         err.value |= 2                       # CTR_GATHER_E_OVERWRITTEN
                     break
+                if time.monotonic() >= deadline:
+                    err.value |= 8                           # CTR_GATHER_E_PREV_TIMEOUT
+                    break
                 time.sleep(0.0005)
-            else:
-                err.value |= 8                               # CTR_GATHER_E_PREV_TIMEOUT
 
     def copy_list(self, plan, streams, ready_event, done_events):
         import ctypes
@@ -242,17 +252,16 @@ class _ShmCopyOps(object):
             assert 0 <= s < len(streams)
             ctypes.memmove(dst, src, nbytes)
 
-    def wait(self, seqw_ptr, n, seq, spin_limit, err, stream):
+    def wait(self, seqw_ptr, n, seq, wait_us, err, stream):
         import ctypes
         import time
         words = (ctypes.c_uint32 * n).from_address(seqw_ptr)
-        for _ in range(spin_limit):
-            if all(((w - seq) & 0xFFFFFFFF) < 0x80000000 for w in words):
-                break
+        deadline = time.monotonic() + wait_us * 1e-6
+        while not all(((w - seq) & 0xFFFFFFFF) < 0x80000000 for w in words):
+            if time.monotonic() >= deadline:
+                err[0] |= 1
+                return
             time.sleep(0.001)
-        else:
-            err[0] |= 1
-            return
         if any(w != seq for w in words):
             err[0] |= 2
 
@@ -271,7 +280,7 @@ def _ce_worker(rank, world, port, n, engine, q):
     try:
         from ctr_reach_amd import distributed as D
         ops = _ShmCopyOps()
-        g = D.PushGather(n, depth=3, engine=engine, n_streams=2, ops=ops, spin_limit=5000)
+        g = D.PushGather(n, depth=3, engine=engine, n_streams=2, ops=ops, wait_us=5_000_000)
 
         def step(seq, packed):
             if engine == "sdma":
@@ -393,7 +402,7 @@ def _flow_worker(rank, world, port, n, steps, mode, q):
         from ctr_reach_amd import distributed as D
         ops = _ShmCopyOps()
         wait_prev = mode in ("wait_prev", "wrap")
-        g = D.PushGather(n, depth=3, engine="fused", ops=ops, spin_limit=20000, wait_prev=wait_prev)
+        g = D.PushGather(n, depth=3, engine="fused", ops=ops, wait_us=10_000_000, wait_prev=wait_prev)
         rng = np.random.default_rng(rank)
         views = []
         first = 1
@@ -471,7 +480,7 @@ def _check_worker(rank, world, port, n, corrupt_at, q):
         import ctypes
         from ctr_reach_amd import distributed as D
         ops = _ShmCopyOps()
-        g = D.PushGather(n, depth=3, engine="fused", ops=ops, spin_limit=20000)
+        g = D.PushGather(n, depth=3, engine="fused", ops=ops, wait_us=10_000_000)
         cur_rows = {}
 
         def step(i):
@@ -519,3 +528,50 @@ def test_push_check_fails_on_every_rank_for_a_corrupted_slot(corrupt_at):
             assert not rep["passed"] and rep["failed_at_step"] == corrupt_at, rep
             assert rep["steps_checked"] == corrupt_at + 1 and rep["mismatched_rows_max"] == 1, rep
             assert not rep["rows_equal_all_ranks"] and rep["err_bits_max"] == 0, rep
+
+
+def _overrun_worker(rank, world, port, n, q):
+    sys.path.insert(0, os.path.join(ROOT, "gym-ctr-reach_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = None
+    try:
+        from ctr_reach_amd import distributed as D
+        ops = _ShmCopyOps()
+        g = D.PushGather(n, depth=3, engine="fused", ops=ops, wait_us=50_000)
+        if rank == 0:
+            # rank 1 never steps (never releases): steps 4 and 5 time out after 50 ms and overwrite
+            # rank 1's unreleased slots
+            for seq in range(1, 6):
+                cur, prev, prev_seq = g.step_args(seq)
+                ops.fused_step(cur, prev, prev_seq, seq, _rows(n, rank, seq))
+                g.stepped(seq)
+        dist.barrier()
+        q.put((rank, g.err_bits(), [int(v) for v in g.poison]))
+        dist.barrier()
+    finally:
+        if g is not None:
+            g.close()
+        dist.destroy_process_group()
+
+
+def test_push_gather_overrun_is_reported_to_the_consumer():
+    """A producer whose release wait times out (the consumer never released the slot) stores its
+    rows anyway: its own err gets CTR_GATHER_E_RELEASE_TIMEOUT, and so does the OVERRUN consumer's,
+    through the producer's poison word in the consumer's memory (PushGather.err_bits) -- a rank can
+    trust its local error bits without a cross-rank reduction."""
+    world, n = 2, 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_overrun_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: (e, pw) for r, e, pw in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] & 4, got
+    assert got[1][0] & 4, got
+    assert got[1][1] == [5, 0], got          # producer 0's last overrun step; rank 1 never produced
+    assert got[0][1] == [0, 0], got          # rank 0 itself was never overrun

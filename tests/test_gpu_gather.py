@@ -124,7 +124,7 @@ def test_push_gather_two_processes_one_gpu(cuda, backend, world):
     for p in procs:
         p.start()
     try:
-        errs = q.get(timeout=240)
+        got = dict(q.get(timeout=240) for _ in range(world))
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -214,18 +214,22 @@ def _stalled_worker(rank, world, port, n, q):
         torch.cuda.set_device(dev)
         env = CtrReachVecEnv(n, device=dev, seed=5, env_base=rank * n, pack_outputs=True)
         env.reset()
-        g = env.enable_gather("push", depth=3, spin_limit=2000)
+        g = env.enable_gather("push", depth=3, wait_us=2000)
         errs = []
         if rank == 0:
             # rank 1 never steps: it never releases a slot, so from step depth + 1 on this rank's
-            # k_step waits for the release, gives up after spin_limit polls, and flags it
+            # k_step waits for the release, gives up after wait_us (2 ms), and flags it
             rng = np.random.default_rng(4)
             for _ in range(5):
                 env.step(_acts(env, rng))
                 torch.cuda.synchronize()
                 errs.append(int(g.err.item()))
-            q.put(errs)
+            q.put((0, errs))
         dist.barrier()
+        if rank == 1:
+            # the overrun consumer learns it from its own error bits (the producer's poison
+            # stores into its memory), without any cross-rank reduction
+            q.put((1, g.err_bits()))
         assert _abi.CTR_GATHER_E_RELEASE_TIMEOUT == 4
         g.close()
     finally:
@@ -235,7 +239,8 @@ def _stalled_worker(rank, world, port, n, q):
 @pytest.mark.timeout(300)
 def test_push_gather_unreleased_slot_times_out_without_hanging(cuda):
     """A consumer that never steps never releases its slots: the producer's k_step stores after a
-    bounded wait and sets CTR_GATHER_E_RELEASE_TIMEOUT (steps 1-3 need no release: depth 3)."""
+    bounded wait and sets CTR_GATHER_E_RELEASE_TIMEOUT (steps 1-3 need no release: depth 3), and
+    the overrun consumer's own err_bits() carry it too (poison words, ABI 14)."""
     import torch.multiprocessing as mp
     world, n = 2, 1024
     port = _free_port()
@@ -245,12 +250,14 @@ def test_push_gather_unreleased_slot_times_out_without_hanging(cuda):
     for p in procs:
         p.start()
     try:
-        errs = q.get(timeout=240)
+        got = dict(q.get(timeout=240) for _ in range(world))
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.exitcode is None:
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
+    errs = got[0]
     assert errs[:3] == [0, 0, 0], errs
     assert errs[3] & 4 and errs[4] & 4, errs
+    assert got[1] & 4, got

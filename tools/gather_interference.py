@@ -71,7 +71,8 @@ if mode == "fused":
         def __init__(self):
             flow = {"relw": [relw + 4 * i for i in range(peers)], "rel": relw,
                     "wait_seqw": [seqw + 4 * peers * ((s - 1) % D) for s in range(D)],
-                    "err": gerr.data_ptr(), "depth": D, "spin_limit": 1 << 22}
+                    "err": gerr.data_ptr(), "depth": D, "wait_us": 10_000_000,
+                    "poisonw": [seqw + 3072 + 4 * i for i in range(peers)], "poison": seqw + 3072}
             self.keep, self.desc = ops.upload_descriptors(
                 [[(ring + (s * peers + i) * block, seqw + 4 * (s * peers + i)) for i in range(peers)] for s in range(D)],
                 n, seqw + 2048, flow)
