@@ -683,7 +683,7 @@ def main():
                                "per map + 63 to apply it + 37 per composition), not at the stepped count"
                                if cfgd["integrator"] == "rk4" else "SURVEY 8(d) count"))},
     }
-    tr = os.path.join(ROOT, "profiles", "traffic.json")
+    tr = os.path.join(ROOT, "profiles", "traffic.json" if args.config == 3 else "traffic_c%d.json" % args.config)
     if ws > 1:
         # the one-GPU PMC passes do not see a rank's stores into its peers' rings (16 B per env and
         # peer) nor RCCL's traffic
@@ -695,7 +695,7 @@ def main():
             t = json.load(fh)
         if t.get("envs") == n and t.get("config", 3) == args.config and systems == [0]:
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
-            out["roofline"]["traffic_source"] = "profiles/traffic.json: " + t.get("note", "")
+            out["roofline"]["traffic_source"] = "profiles/%s: %s" % (os.path.basename(tr), t.get("note", ""))
             out["roofline"]["traffic_over_algorithmic"] = t.get("bytes_per_launch") / (BYTES_STEP * n)
     if not args.no_cpu_baseline and ws == 1:
         out["parity"] = parity_probe(env, cfgd)

@@ -12,6 +12,7 @@
 #   profile   scripts/profile.sh $TAG (kernel trace + PMC passes; tools/summarize_profile.py $TAG here)
 #   traffic   k_step / k_refill FETCH_SIZE and WRITE_SIZE at the bench's --steps 20, with the
 #             default refill budget and with --refill-budget 0
+#   tattrib   k_step reads by source: FETCH_SIZE / WRITE_SIZE passes of tools/traffic_attrib.py
 #   fake      RCCL-footprint stand-in (tools/fake_gather.hip, built here into tools/libfake_gather.so)
 #             at 2-32 workgroups, durations from a per-channel bandwidth model
 #   refill    k_refill timed alone per refill budget (tools/time_refill_budget.py)
@@ -84,6 +85,14 @@ traffic)
     pmc r4t_fetch_b0 FETCH_SIZE --steps 20 --warmup 5 --profile-only --refill-budget 0
     pmc r4t_write_b0 WRITE_SIZE --steps 20 --warmup 5 --profile-only --refill-budget 0
     ;;
+tattrib)
+    # k_step reads by source (tools/traffic_attrib.py): one FETCH_SIZE and one WRITE_SIZE pass
+    timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/tra_fetch -o run -- \
+        python3 tools/traffic_attrib.py run > gpurun_out/tra_fetch.log 2>&1 || { echo "tra_fetch failed"; tail -5 gpurun_out/tra_fetch.log; exit 1; }
+    timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/tra_write -o run -- \
+        python3 tools/traffic_attrib.py run > gpurun_out/tra_write.log 2>&1 || { echo "tra_write failed"; tail -5 gpurun_out/tra_write.log; exit 1; }
+    echo "tattrib ok"
+    ;;
 fake)
     # 7.3 MB received per GPU and step (7 x 65 536 x 16 B) at ~40 GB/s per channel
     for wd in "2 92" "4 46" "8 23" "16 12" "32 6"; do
@@ -128,7 +137,7 @@ tailprobe)
     done
     ;;
 *)
-    echo "usage: bash scripts/gpu.sh suite|bench|evidence|soak|pushsoak|interf|profile|traffic|fake|refill|ab|abt|wavet|pmcab|tailprobe ..."
+    echo "usage: bash scripts/gpu.sh suite|bench|evidence|soak|pushsoak|interf|profile|traffic|tattrib|fake|refill|ab|abt|wavet|pmcab|tailprobe ..."
     exit 2 ;;
 esac
 done

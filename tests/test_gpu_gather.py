@@ -124,7 +124,7 @@ def test_push_gather_two_processes_one_gpu(cuda, backend, world):
     for p in procs:
         p.start()
     try:
-        got = dict(q.get(timeout=240) for _ in range(world))
+        errs = q.get(timeout=240)
     finally:
         for p in procs:
             p.join(timeout=30)

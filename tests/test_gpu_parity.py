@@ -382,6 +382,53 @@ def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand, budg
         assert b.sweeps > 0
 
 
+@pytest.mark.parametrize("event", ["sweep", "restore"])
+def test_carried_resets_survive_sweeps_and_requeues(cuda, event):
+    """The resumable refill's suspended resets across the two events that move an env past them
+    (ADVICE r4): "sweep" -- the ring is emptied and the steps run the miss sweep, so done envs take
+    synchronous resets and pass reset numbers still suspended on the carry lists (k_refill must
+    drop those rather than write them into a slot), then a requeue refills the ring; "restore" --
+    a checkpoint restore while resets are suspended (k_pool_requeue empties the carry lists and
+    queues them again).  Every step stays bit-identical to synchronous resets and no pooled step
+    misses."""
+    import torch
+    from ctr_reach_amd import _abi
+    n = 2048
+    kw = dict(seed=17, max_steps_per_episode=3, select_systems=[0, 1, 2, 3])
+    a = _env(cuda, n, pool_depth=0, **kw)
+    b = _env(cuda, n, pool_depth=24, refill_interval=4, refill_budget=1, **kw)
+    assert b.carry is not None
+    a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03
+    a.reset(); b.reset()
+    rng = np.random.default_rng(9)
+    carried_at_event = None
+    for i in range(22):
+        if i == 6:
+            carried_at_event = sum(b.carried())
+            if event == "sweep":
+                b.pool_r.zero_()                 # the ring holds nothing: misses, swept
+                b._pool_full = False
+            else:
+                a.load_state_dict(a.state_dict())
+                b.load_state_dict(b.state_dict())
+                assert b._pool_full
+        if event == "sweep" and i == 14:
+            b._requeue_pool()                    # back to a full ring (carry lists emptied, requeued)
+            assert b._pool_full
+        act = torch.tensor((rng.uniform(-1, 1, (n, 6)) * a.action_space.high).astype(np.float32), device=cuda)
+        a.step(act)
+        b.step(act)
+        torch.cuda.synchronize()
+        for k in ("joints", "desired_goal", "achieved_goal", "t", "system", "epoch", "obs", "terminal_obs"):
+            np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(),
+                                          err_msg="%s at step %d" % (k, i))
+        assert not (b.status.cpu().numpy() & _abi.CTR_STATUS_POOL_MISS).any(), i
+    assert carried_at_event > 0
+    assert (a.epoch.cpu().numpy() >= 5).all()
+    if event == "sweep":
+        assert b.sweeps >= 8
+
+
 def test_pooled_autoreset_broken_promise_is_flagged(cuda):
     """CTR_AUTORESET_POOLED on a pool that does NOT hold the next resets (the caller's promise
     broken): done envs are flagged CTR_STATUS_POOL_MISS and keep their state (no reset, t counts
