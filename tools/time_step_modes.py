@@ -1,6 +1,6 @@
 """Diagnostic: k_step time (HIP events, 100 back-to-back launches after 300 warm ones) for the
 library named by CTR_REACH_AMD_LIB, with auto-reset off and with the pooled auto-reset.
-usage: python tools/time_step_modes.py [n_envs] [rigid]"""
+usage: python tools/time_step_modes.py [n_envs] [rigid|c5]"""
 import os
 import sys
 
@@ -14,6 +14,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 kw = {}
 if len(sys.argv) > 2 and sys.argv[2] == "rigid":      # configs[1]: rigid model, RK4 at 100 steps/m
     kw = dict(integrator="rk4", rk4_steps_per_m=100, model="rigid")
+if len(sys.argv) > 2 and sys.argv[2] == "c5":         # configs[4]: compliant model, RK4 at 400 steps/m
+    kw = dict(integrator="rk4", rk4_steps_per_m=400, model="compliant")
 env = CtrReachVecEnv(n, device="cuda", seed=0, refill_interval=64, **kw)
 env.reset()
 g = torch.Generator(device="cuda")
