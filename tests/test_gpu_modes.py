@@ -193,3 +193,25 @@ def test_nan_and_far_joints_terminate(cuda, integrator, spm, model):
     env.joints.copy_(torch.tensor(q, device=cuda))
     env.step(torch.zeros((4, 6), device=cuda))
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("integrator,spm,model", MODES + [("rk45_scipy", 100, "compliant")])
+def test_fk_is_independent_of_wave_composition(cuda, oracle_mod, integrator, spm, model):
+    """A lane's FK must not depend on which envs share its wave: the kernels pick a code path per
+    wave (tube levels, the careful trig, the RK4 step level), so every path must give a lane the
+    same bits -- the property the shard test, pooled-vs-synchronous resets and the refill's
+    arbitrary lane pairing rest on.  The same joints in a permuted order (other wave mates) give
+    bit-identical tips, RHS counts and status words; systems mixed, angles up to +-10 rad."""
+    import torch
+    from ctr_reach_amd import CtrReachVecEnv
+    q, sysid = _joints(oracle_mod, 16384, 33)
+    env = CtrReachVecEnv(1, device=cuda, select_systems=[0, 1, 2, 3], integrator=integrator,
+                         rk4_steps_per_m=spm, model=model)
+    tip, st = env.forward_kinematics(q, sysid, return_stats=True)
+    perm = np.random.default_rng(5).permutation(q.shape[0])
+    tip_p, st_p = env.forward_kinematics(q[perm], sysid[perm], return_stats=True)
+    inv = np.argsort(perm)
+    np.testing.assert_array_equal(tip_p.cpu().numpy()[inv], tip.cpu().numpy())
+    for k in ("nfev", "nstep", "nrej", "nseg", "status"):
+        np.testing.assert_array_equal(st_p[k].cpu().numpy()[inv], st[k].cpu().numpy(), err_msg=k)
+    torch.cuda.synchronize()
