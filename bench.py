@@ -666,7 +666,10 @@ def main():
                      "kernel_ms_autoreset_pooled_note": ("k_step as the window launches it (CTR_AUTORESET_POOLED: done "
                                                          "envs copy their precomputed reset), %d back-to-back launches "
                                                          "after the window, no refill among them; its frac prices the "
-                                                         "same FK work as kernel_ms" % (R_steps - 1)),
+                                                         "same FK work as kernel_ms" % (R_steps - 1)
+                                                         if k_ms_pooled else
+                                                         "not measured: the window's steps also run the per-step gather "
+                                                         "(or a refill period of one step)"),
                      "flops_per_launch": flops_env_step, "sincos_per_launch": sincos,
                      "nfev_per_env_step": nfev_mean,
                      "bytes_per_launch_algorithmic": BYTES_STEP * n,
