@@ -95,9 +95,11 @@ def parse():
                     help="replay each refill period's steps from one captured HIP graph (CtrReachVecEnv."
                          "capture_steps) instead of launching step by step from Python; auto: on without the "
                          "per-step gather")
+    ap.add_argument("--pool-depth", type=int, default=None,
+                    help="reset pool slots per env (default: the env's for the refill interval and budget)")
     ap.add_argument("--refill-budget", type=int, default=None,
-                    help="resumable refill: RK45 iterations per reset FK and refill (default: the env's, 6; "
-                         "0 = every refill runs its FKs to the end)")
+                    help="resumable refill: RK45 iterations (RK4 steps) per reset FK and refill (default: the "
+                         "env's, 6 (32); 0 = every refill runs its FKs to the end)")
     ap.add_argument("--obs-dtype", choices=("float32", "float64"), default="float32",
                     help="stored observation dtype (computed in float64 either way; float64 = the reference's)")
     ap.add_argument("--dry-run", action="store_true",
@@ -375,7 +377,8 @@ def main():
     env = CtrReachVecEnv(n, device=dev, seed=args.seed, env_base=D.shard(n, rank), autoreset=True, record_info=False,
                          integrator=cfgd["integrator"], rk4_steps_per_m=cfgd["rk4_steps_per_m"], model=cfgd["model"],
                          select_systems=systems, refill_interval=R, pack_outputs=gather, obs_dtype=args.obs_dtype,
-                         refill_budget=args.refill_budget if cfgd["integrator"] == "rk45_scipy" else None)
+                         refill_budget=args.refill_budget if cfgd["model"] == "compliant" else None,
+                         pool_depth=args.pool_depth)
     env.reset()
     max_steps = env.max_steps_per_episode
     if not args.no_stagger:

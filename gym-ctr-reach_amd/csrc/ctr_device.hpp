@@ -1330,21 +1330,30 @@ __device__ __forceinline__ Rk4Plan rk4_plan(const Seg &sg, double *end_lds, int 
     return pl;
 }
 
-template <bool HAS_UY, bool RIGID, bool CAREFUL = true>
-__device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], FkStats &st, double steps_per_m)
+// RESUME (the pool refill, compliant model): start from *from when it is non-null, and after
+// `budget` RK4 steps suspend into *to and return false (true = tip written).  The suspended state
+// is y, the gap cursor (the remaining stepped gaps, the current one and its steps left) and the
+// counters; the plan is a pure function of the joints and is rebuilt on resume, so a suspended-
+// and-resumed FK is bit-identical to an uninterrupted one (FkSuspend: remaining, k, flags = steps
+// left).
+template <bool HAS_UY, bool RIGID, bool CAREFUL = true, bool RESUME = false>
+__device__ bool fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], FkStats &st, double steps_per_m,
+                            const FkSuspend *from = nullptr, FkSuspend *to = nullptr, int budget = 0)
 {
     constexpr bool LEVELS = !HAS_UY && !RIGID;
+    static_assert(!RESUME || !RIGID, "the rigid model's FKs run as segment maps, nothing to suspend");
     const double beta[3] = {q[0], q[1], q[2]};
     double *end_lds = &s_seg_end[0][threadIdx.x];
     int *n_lds = &s_seg_n[0][threadIdx.x];
     const Seg sg = seg_build(sy, beta, end_lds);
     const Rk4Plan pl = rk4_plan<LEVELS, RIGID>(sg, end_lds, n_lds, steps_per_m);
-    st.nseg += (uint32_t)__builtin_popcount(sg.kept);
     double yu[3] = {0.0, 0.0, 0.0};
     double ya[3] = {q[3], q[4], q[5]};
     double yr[3] = {0.0, 0.0, 0.0};
     double yR[9];
-    {
+    const bool resumed = RESUME && from != nullptr;
+    if (!resumed) {
+        st.nseg += (uint32_t)__builtin_popcount(sg.kept);
         double s0, c0;
         sincos_lds(ya[0], s0, c0);
         yR[0] = c0; yR[1] = -s0; yR[2] = 0.0;
@@ -1359,11 +1368,44 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
         int left = 0;                         // steps left in the current gap
         bool lv3 = true;
         uint32_t rem = pl.step;
+        int kcur = 0, iters = 0;              // RESUME: the current gap, steps run here
+        if constexpr (RESUME) {
+            if (resumed) {
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) { yu[i] = from->yu[i]; ya[i] = from->ya[i]; yr[i] = from->yr[i]; }
+                #pragma unroll
+                for (int i = 0; i < 9; ++i) yR[i] = from->yR[i];
+                rem = from->remaining;
+                kcur = (int)from->k;
+                left = (int)from->flags;
+                st = from->st;
+                if (left > 0) {
+                    p = seg_par_at<HAS_UY, false>(sy, seg_bits(sg, kcur));
+                    h = end_lds[kcur * CTR_BLOCK];
+                    lv3 = (p.present & 4u) != 0u || p.present == 0u;
+                }
+            }
+        }
         for (;;) {
+            if constexpr (RESUME) {
+                if (iters >= budget && (left > 0 || rem != 0u)) {
+                    #pragma unroll
+                    for (int i = 0; i < 3; ++i) { to->yu[i] = yu[i]; to->ya[i] = ya[i]; to->yr[i] = yr[i]; }
+                    #pragma unroll
+                    for (int i = 0; i < 9; ++i) to->yR[i] = yR[i];
+                    to->remaining = rem;
+                    to->k = (uint32_t)kcur;
+                    to->flags = (uint32_t)left;
+                    to->st = st;
+                    return false;
+                }
+                ++iters;
+            }
             if (left == 0) {
                 if (rem == 0u) break;
                 const int k = __builtin_ctz(rem);
                 rem &= rem - 1u;
+                if constexpr (RESUME) kcur = k;
                 p = seg_par_at<HAS_UY, false>(sy, seg_bits(sg, k));
                 h = end_lds[k * CTR_BLOCK];
                 left = n_lds[k * CTR_BLOCK];
@@ -1415,6 +1457,7 @@ __device__ void fk_lane_rk4(const SysK &sy, const double q[6], double tip[3], Fk
     }
     tip[0] = yr[0]; tip[1] = yr[1]; tip[2] = yr[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+    return true;
 }
 
 // Rigid model + fixed-step RK4 with one env on a group of SEG_GROUP consecutive lanes (k_step for

@@ -1139,15 +1139,22 @@ struct CarryHdr {
 };
 static_assert(sizeof(CarryHdr) == 1024, "CarryHdr layout");
 
-// One FK of a refill: the scipy-RK45 FK runs at most `budget` iterations and can start from a
-// suspended state (fk_lane RESUME); fixed-step RK4 always runs to the end.
+// One FK of a refill: the scipy-RK45 FK runs at most `budget` iterations (the compliant RK4 FK
+// at most `budget` RK4 steps) and can start from a suspended state (fk_lane / fk_lane_rk4
+// RESUME); the rigid model's segment maps always run to the end.
 template <int MODE>
 __device__ __forceinline__ bool fk_refill(const KCfg &kc, const SysK &sy, const float q[6], double tip[3], FkStats &st,
                                           const FkSuspend *from, FkSuspend *to, int budget)
 {
-    if constexpr ((MODE & 2) != 0) {
+    if constexpr ((MODE & 4) != 0) {
         fk_dispatch<MODE>(kc, sy, q, tip, st);
         return true;
+    } else if constexpr ((MODE & 2) != 0) {
+        constexpr bool UY = (MODE & 1) != 0;
+        const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
+        const double spm = (double)kc.c.rk4_steps_per_m;
+        if (fk_needs_careful_trig(qd)) return fk_lane_rk4<UY, false, true, true>(sy, qd, tip, st, spm, from, to, budget);
+        return fk_lane_rk4<UY, false, false, true>(sy, qd, tip, st, spm, from, to, budget);
     } else {
         constexpr bool UY = (MODE & 1) != 0, RG = (MODE & 4) != 0;
         const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
@@ -1163,7 +1170,7 @@ __device__ __forceinline__ bool fk_refill(const KCfg &kc, const SysK &sy, const 
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
-    constexpr bool RESUMABLE = (MODE & 2) == 0;
+    constexpr bool RESUMABLE = (MODE & 4) == 0;           // scipy RK45 and compliant RK4
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int64_t s_count, s_carried;

@@ -27,6 +27,7 @@ from .systems import default_kwargs, make_config, solver_codes, tubes_from_param
 NUM_TUBES = 3
 EXT_TOL = 1e-3    # obs.py:14
 ZERO_TOL = 1e-4   # obs.py:16
+RK4_REFILL_BUDGET = 32   # resumable refill, fixed-step RK4: RK4 steps per reset FK and refill
 
 
 def _torch():
@@ -176,17 +177,18 @@ class CtrReachVecEnv(object):
         # precomputed in batches every `refill_interval` steps and consumed by a copy
         # depth >= the refill interval: every env then finds its next reset in the pool on every
         # step (CTR_AUTORESET_POOLED, no miss-sweep launch); 108 B per env and slot
-        # resumable refill (scipy RK45 only): a reset at least one refill period ahead of its env
-        # runs at most refill_budget iterations of each FK per refill; an unfinished one is
+        # resumable refill (scipy RK45, and fixed-step RK4 on the compliant model): a reset at least
+        # one refill period ahead of its env runs at most refill_budget iterations (RK45 attempts,
+        # RK4 steps) of each FK per refill; an unfinished one is
         # suspended and resumed (bit-identically) by the next refill, so a refill lasts about as
         # long as the budget instead of its slowest fresh sample's FK (ctr_batch_t.carry).  The
         # resets less than a period ahead always finish: none is due before it lands
         R = max(1, int(refill_interval))
-        resumable = integrator == "rk45_scipy"
+        resumable = integrator == "rk45_scipy" or model == "compliant"
         if refill_budget is None:
-            refill_budget = 6 if resumable else 0
+            refill_budget = (6 if integrator == "rk45_scipy" else RK4_REFILL_BUDGET) if resumable else 0
         if refill_budget and not resumable:
-            raise ValueError("refill_budget needs the scipy RK45 integrator")
+            raise ValueError("refill_budget needs the compliant model (the rigid model's FKs run as segment maps)")
         if pool_depth is None:
             # deep enough for the budget to apply over about two refills (queued resets are
             # P - R - 1 or more ahead); 64 slots cap the ring (108 B per env and slot)

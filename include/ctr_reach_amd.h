@@ -162,17 +162,18 @@ typedef struct ctr_batch_t {
     int32_t  *refill;            /* [2 + 2 refill_cap]: count, (env, reset number) pairs,
                                     then a completion ticket (zero-initialised)          */
     int64_t   refill_cap;
-    /* Resumable refill (optional, carry NULL disables it; scipy-RK45 integrator only).  A
-     * reset at least refill_lead resets ahead of its environment (r - epoch - 1 >= refill_lead
-     * at the time of the refill) runs at most refill_budget iterations (segment start + RK45
-     * attempt) of each of its two FKs in one ctr_pool_refill; an unfinished one is suspended
+    /* Resumable refill (optional, carry NULL disables it; scipy RK45, and fixed-step RK4 on the
+     * compliant model -- the rigid model's segment maps ignore it).  A reset at least
+     * refill_lead resets ahead of its environment (r - epoch - 1 >= refill_lead at the time of
+     * the refill) runs at most refill_budget iterations (segment start + RK45 attempt; one RK4
+     * step) of each of its two FKs in one ctr_pool_refill; an unfinished one is suspended
      * into the carry list and resumed by the next ctr_pool_refill, which writes its pool slot
      * once both FKs are done.  The result is bit-identical; only the refill a reset lands in
      * changes.  With refill_lead >= the steps between refills, no reset is due before it lands
      * (after every refill, the resets fewer than refill_lead ahead are in the pool).  */
     void     *carry;             /* ctr_refill_carry_bytes(carry_cap) B, zero-initialised */
     int64_t   carry_cap;         /* resets each of its two lists holds                 */
-    int32_t   refill_budget;     /* iterations per FK and refill (0 = no budget)      */
+    int32_t   refill_budget;     /* iterations (RK4 steps) per FK and refill (0 = none) */
     int32_t   refill_lead;
 } ctr_batch_t;
 

@@ -352,13 +352,28 @@ def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand, budg
     still take (an intermittent mixed-slot race before that rule).
     depth > 2 interval (the resumable refill): resets suspended by one refill land with the next,
     never after they are due (no sweep, no CTR_STATUS_POOL_MISS) and bit-identical."""
+    _pool_parity(cuda, depth, interval, rand, budget)
+
+
+@pytest.mark.parametrize("model,depth,interval,rand,budget", [
+    ("compliant", None, 4, 0.0, None), ("compliant", None, 4, 0.05, 3), ("compliant", 16, 3, 0.0, 7),
+    ("compliant", 4, 8, 0.0, None), ("rigid", None, 4, 0.0, None), ("rigid", 2, 3, 0.05, None)])
+def test_rk4_reset_pool_matches_synchronous_resets(cuda, model, depth, interval, rand, budget):
+    """The same parity on fixed-step RK4 (BASELINE configs[4]'s 400 steps per metre): the
+    compliant model's refill suspends FKs after `budget` RK4 steps (mid-gap: the state, the gap
+    cursor and its steps left) and the next refill finishes them bit-identically; the rigid
+    model's segment-map FKs always finish in their refill (no carry lists)."""
+    _pool_parity(cuda, depth, interval, rand, budget, integrator="rk4", rk4_steps_per_m=400, model=model)
+
+
+def _pool_parity(cuda, depth, interval, rand, budget, **solver):
     import torch
     n = 4096
-    kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3], domain_rand=rand)
+    kw = dict(seed=11, max_steps_per_episode=4, select_systems=[0, 1, 2, 3], domain_rand=rand, **solver)
     a = _env(cuda, n, pool_depth=0, **kw)
     b = _env(cuda, n, pool_depth=depth, refill_interval=interval, refill_budget=budget, **kw)
     resumable = b.carry is not None
-    assert resumable == (b.pool_depth > 2 * interval)
+    assert resumable == (b.pool_depth > 2 * interval and solver.get("model", "compliant") == "compliant")
     a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03   # plenty of early successes
     a.reset(); b.reset()
     rng = np.random.default_rng(4)
@@ -391,12 +406,23 @@ def test_carried_resets_survive_sweeps_and_requeues(cuda, event):
     a checkpoint restore while resets are suspended (k_pool_requeue empties the carry lists and
     queues them again).  Every step stays bit-identical to synchronous resets and no pooled step
     misses."""
+    _carried_resets_events(cuda, event)
+
+
+@pytest.mark.parametrize("event", ["sweep", "restore"])
+def test_carried_rk4_resets_survive_sweeps_and_requeues(cuda, event):
+    """The same two events with the compliant model's fixed-step RK4 FKs suspended mid-gap (the
+    RK4 resumable refill: RK4 steps as the budget's unit)."""
+    _carried_resets_events(cuda, event, integrator="rk4", rk4_steps_per_m=400, refill_budget=5)
+
+
+def _carried_resets_events(cuda, event, refill_budget=1, **solver):
     import torch
     from ctr_reach_amd import _abi
     n = 2048
-    kw = dict(seed=17, max_steps_per_episode=3, select_systems=[0, 1, 2, 3])
+    kw = dict(seed=17, max_steps_per_episode=3, select_systems=[0, 1, 2, 3], **solver)
     a = _env(cuda, n, pool_depth=0, **kw)
-    b = _env(cuda, n, pool_depth=24, refill_interval=4, refill_budget=1, **kw)
+    b = _env(cuda, n, pool_depth=24, refill_interval=4, refill_budget=refill_budget, **kw)
     assert b.carry is not None
     a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03
     a.reset(); b.reset()
