@@ -3,7 +3,10 @@ step, pooled auto-resets (several ring depths / refill intervals, domain randomi
 synchronous resets, every state array compared bit for bit every 10 steps.  A longer cousin of
 tests/test_gpu_parity.py::test_reset_pool_matches_synchronous_resets for rare races.  The last
 configurations run the resumable refill (pool depth > 2 x interval: FKs suspended after `budget`
-iterations and resumed by later refills); no CTR_STATUS_POOL_MISS may appear."""
+iterations and resumed by later refills); no CTR_STATUS_POOL_MISS may appear.
+
+usage: python tools/soak_pool.py [rk4]   (rk4: BASELINE configs[4]'s compliant fixed-step RK4 at
+400 steps per metre, its FKs suspended mid-gap after `budget` RK4 steps)"""
 import os
 import sys
 
@@ -14,12 +17,16 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from ctr_reach_amd import CtrReachVecEnv  # noqa: E402
 cuda = torch.device("cuda", 0)
 n = 8192
+rk4 = len(sys.argv) > 1 and sys.argv[1] == "rk4"
+solver = dict(integrator="rk4", rk4_steps_per_m=400) if rk4 else {}
 configs = [(0, 1, 0.0, 0), (2, 3, 0.0, 0), (1, 4, 0.05, 0), (3, 7, 0.0, 0), (5, 5, 0.05, 0), (8, 4, 0.0, 0),
            (None, 4, 0.0, 6), (None, 2, 0.05, 3), (40, 5, 0.0, 2), (None, 10, 0.0, 6)]
+if rk4:
+    configs = configs[:3] + [(None, 4, 0.0, 32), (None, 2, 0.05, 5), (40, 5, 0.0, 11), (None, 10, 0.0, None)]
 bad = 0
 for depth, interval, rand, budget in configs:
     kw = dict(seed=5 + (depth or 0), max_steps_per_episode=5, select_systems=[0, 1, 2, 3], domain_rand=rand,
-              refill_budget=budget)
+              refill_budget=budget, **solver)
     a = CtrReachVecEnv(n, device=cuda, pool_depth=0, **kw)
     b = CtrReachVecEnv(n, device=cuda, pool_depth=depth, refill_interval=interval, **kw) if depth != 0 else \
         CtrReachVecEnv(n, device=cuda, pool_depth=8, refill_interval=3, **kw)
