@@ -5,7 +5,7 @@
 #   bench     headline bench x2 (+ CPU baseline once) and the two-rank gloo rehearsal on one GPU
 #             (exercises the push gather's pre-window check, calibration and post-window check)
 #   evidence  every bench line: headline x2, 128 steps, float64 observations, configs[1] x2,
-#             configs[4], mixed systems 0-3
+#             configs[4] (20 and 128 steps), mixed systems 0-3
 #   soak      reset-pool soak (tools/soak_pool.py: pooled vs synchronous resets, bit-equal)
 #   pushsoak  fused-push flow-control soak: $WORLD free-running ranks on one GPU (tools/push_soak.py)
 #   interf    fused push into 8 blocks on one GPU: per-step cost with and without the fused wait
@@ -62,6 +62,7 @@ evidence)
     run bench_c2 300 python bench.py --config 2 --steps 20 --warmup 5 --cpu-seconds 5
     run bench_c2b 300 python bench.py --config 2 --steps 20 --warmup 5 --no-cpu-baseline
     run bench_c5 300 python bench.py --config 5 --steps 20 --warmup 5 --cpu-seconds 5
+    run bench_c5_128 300 python bench.py --config 5 --warmup 5 --no-cpu-baseline
     run bench_mixed 300 python bench.py --systems 0,1,2,3 --steps 20 --warmup 5 --cpu-seconds 5
     ;;
 soak)
