@@ -1,5 +1,6 @@
 """Diagnostic: k_step time (HIP events, 100 back-to-back launches after 300 warm ones) for the
-library named by CTR_REACH_AMD_LIB, with auto-reset off and with the pooled auto-reset.
+library named by CTR_REACH_AMD_LIB, with auto-reset off and with the pooled auto-reset; then the
+FK operator alone (ctr_fk) on the same joints.
 usage: python tools/time_step_modes.py [n_envs] [rigid|c5]"""
 import os
 import sys
@@ -39,3 +40,14 @@ for mode, name in ((0, "autoreset off"), (_abi.AUTORESET_POOLED, "pooled auto-re
     e1.record(stream)
     torch.cuda.synchronize()
     print("%-20s k_step %.2f us" % (name, e0.elapsed_time(e1) / 100 * 1e3), flush=True)
+# the FK operator alone (ctr_fk: k_fk) on the batch's current joints, same clocks
+q = env.joints.clone()
+for i in range(100):
+    env.forward_kinematics(q)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(stream)
+for i in range(100):
+    env.forward_kinematics(q)
+e1.record(stream)
+torch.cuda.synchronize()
+print("%-20s k_fk   %.2f us" % ("FK operator", e0.elapsed_time(e1) / 100 * 1e3), flush=True)
