@@ -1414,12 +1414,20 @@ __global__ __launch_bounds__(BLOCK) void k_pool_requeue(ctr_batch_t b)
     const bool in = e < b.n;
     const uint32_t r = in ? b.epoch[e] : 0u;
     const int P = b.pool_depth;
-    uint64_t miss = 0;                 // bit j - 1: reset r + j missing (P <= 64)
-    for (int j = 1; j <= P && in; ++j) {
-        const uint32_t rr = r + (uint32_t)j;
-        if (b.pool_r[(int64_t)(rr % (uint32_t)P) * b.n + e] != rr) miss |= 1ull << (j - 1);
+    // bit j of word w: reset r + 1 + 64 w + j missing (P <= CTR_POOL_MAX = 3 x 64)
+    uint64_t miss[CTR_POOL_MAX / 64];
+    #pragma unroll
+    for (int w = 0; w < CTR_POOL_MAX / 64; ++w) {
+        uint64_t m = 0;
+        for (int j = 0; j < 64 && 64 * w + j < P && in; ++j) {
+            const uint32_t rr = r + 1u + (uint32_t)(64 * w + j);
+            if (b.pool_r[(int64_t)(rr % (uint32_t)P) * b.n + e] != rr) m |= 1ull << j;
+        }
+        miss[w] = m;
     }
-    const int cnt = __popcll(miss);
+    int cnt = 0;
+    #pragma unroll
+    for (int w = 0; w < CTR_POOL_MAX / 64; ++w) cnt += __popcll(miss[w]);
     const int lane = threadIdx.x & 63;
     int incl = cnt;                    // inclusive prefix sum over the wave
     #pragma unroll
@@ -1432,10 +1440,12 @@ __global__ __launch_bounds__(BLOCK) void k_pool_requeue(ctr_batch_t b)
     int base = 0;
     if (lane == 0) base = atomicAdd(b.refill, total);
     base = __shfl(base, 0) + (incl - cnt);
-    for (uint64_t m = miss; m; m &= m - 1, ++base) {
-        if (base >= b.refill_cap) break;
-        b.refill[1 + 2 * base] = (int32_t)e;
-        b.refill[2 + 2 * base] = (int32_t)(r + 1u + (uint32_t)__builtin_ctzll(m));
+    #pragma unroll
+    for (int w = 0; w < CTR_POOL_MAX / 64; ++w) {
+        for (uint64_t m = miss[w]; m && base < b.refill_cap; m &= m - 1, ++base) {
+            b.refill[1 + 2 * base] = (int32_t)e;
+            b.refill[2 + 2 * base] = (int32_t)(r + 1u + (uint32_t)(64 * w + __builtin_ctzll(m)));
+        }
     }
 }
 
@@ -1490,7 +1500,8 @@ int check_batch(const ctr_batch_t &b, const char *who)
     if (b.n == 0) return 0;
     if (!b.joints || !b.desired_goal || !b.achieved_goal || !b.t || !b.system || !b.epoch)
         return fail(CTR_EINVAL, who);
-    if (b.pool_depth < 0 || b.pool_depth > 64) return fail(CTR_EINVAL, "pool_depth out of range (0..64)");
+    if (b.pool_depth < 0 || b.pool_depth > CTR_POOL_MAX)
+        return fail(CTR_EINVAL, "pool_depth out of range (0..CTR_POOL_MAX = 192)");
     if (b.pool_depth > 0 && (!b.pool_qd || !b.pool_dg || !b.pool_q0 || !b.pool_ag || !b.pool_sys || !b.pool_r ||
                              !b.pool_stat || !b.refill || b.refill_cap <= 0))
         return fail(CTR_EINVAL, "pool_depth > 0 needs every pool buffer and a refill queue");

@@ -14,6 +14,7 @@ CTR_ABI_VERSION = 14
 CTR_IPC_HANDLE_BYTES = 64
 CTR_GATHER_MAX_RANKS = 16
 CTR_MAX_SYSTEMS = 8
+CTR_POOL_MAX = 192          # ctr_batch_t.pool_depth limit
 CTR_HER_SCAN_TILE = 1024
 CTR_INTEGRATOR_RK45_SCIPY = 0
 CTR_INTEGRATOR_RK4 = 1

@@ -48,6 +48,7 @@ extern "C" {
 
 #define CTR_ABI_VERSION 14
 #define CTR_MAX_SYSTEMS 8
+#define CTR_POOL_MAX 192          /* ctr_batch_t.pool_depth limit (reset slots per environment) */
 #define CTR_EINVAL (-1)
 #define CTR_EHIP (-2)
 
@@ -150,7 +151,7 @@ typedef struct ctr_batch_t {
      * of env e holds reset number r (pool_r), precomputed by ctr_pool_refill; an auto-reset
      * consumes it with a copy instead of two forward-kinematics solves.  A missing slot falls
      * back to computing the reset in the same ctr_step call.  Layout [P][n][k]. */
-    int32_t   pool_depth;        /* P (0 = no pool, at most 64)                       */
+    int32_t   pool_depth;        /* P (0 = no pool, at most CTR_POOL_MAX)             */
     int32_t   pool_pad;
     float    *pool_qd;           /* [P][n][6] desired joints                          */
     double   *pool_dg;           /* [P][n][3] desired goal                            */

@@ -341,7 +341,9 @@ def test_refill_writes_only_resets_the_env_can_take(cuda):
     (4, 8, 0.0, None), (1, 1000, 0.0, None), (2, 3, 0.0, None), (4, 8, 0.05, None), (8, 4, 0.0, None),
     (5, 5, 0.05, None), (1, 4, 0.0, None), (2, 7, 0.0, None),
     # resumable refill (P > 2R): FKs suspended after `budget` iterations, finished by the next refill
-    (None, 4, 0.0, None), (None, 4, 0.05, 1), (16, 3, 0.0, 3), (None, 1, 0.0, 1)])
+    (None, 4, 0.0, None), (None, 4, 0.05, 1), (16, 3, 0.0, 3), (None, 1, 0.0, 1),
+    # a ring deeper than 64 slots (k_pool_requeue's miss words beyond the first)
+    (100, 4, 0.0, 2)])
 def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand, budget):
     """Pooled auto-resets (precomputed ahead of time, consumed by a copy; including pool misses
     that fall back to the synchronous path) give bit-identical trajectories to computing every
@@ -357,7 +359,8 @@ def test_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand, budg
 
 @pytest.mark.parametrize("model,depth,interval,rand,budget", [
     ("compliant", None, 4, 0.0, None), ("compliant", None, 4, 0.05, 3), ("compliant", 16, 3, 0.0, 7),
-    ("compliant", 4, 8, 0.0, None), ("rigid", None, 4, 0.0, None), ("rigid", 2, 3, 0.05, None)])
+    ("compliant", 4, 8, 0.0, None), ("rigid", None, 4, 0.0, None), ("rigid", 2, 3, 0.05, None),
+    ("compliant", 150, 3, 0.05, 5)])
 def test_rk4_reset_pool_matches_synchronous_resets(cuda, model, depth, interval, rand, budget):
     """The same parity on fixed-step RK4 (BASELINE configs[4]'s 400 steps per metre): the
     compliant model's refill suspends FKs after `budget` RK4 steps (mid-gap: the state, the gap

@@ -20,7 +20,7 @@ n = 8192
 rk4 = len(sys.argv) > 1 and sys.argv[1] == "rk4"
 solver = dict(integrator="rk4", rk4_steps_per_m=400) if rk4 else {}
 configs = [(0, 1, 0.0, 0), (2, 3, 0.0, 0), (1, 4, 0.05, 0), (3, 7, 0.0, 0), (5, 5, 0.05, 0), (8, 4, 0.0, 0),
-           (None, 4, 0.0, 6), (None, 2, 0.05, 3), (40, 5, 0.0, 2), (None, 10, 0.0, 6)]
+           (None, 4, 0.0, 6), (None, 2, 0.05, 3), (40, 5, 0.0, 2), (None, 10, 0.0, 6), (130, 5, 0.0, 3)]
 if rk4:
     configs = configs[:3] + [(None, 4, 0.0, 32), (None, 2, 0.05, 5), (40, 5, 0.0, 11), (None, 10, 0.0, None)]
 bad = 0
