@@ -633,7 +633,7 @@ __device__ __forceinline__ void rk45_attempt_lv(const SegPar &p, double yu[3], d
     }
     Stage K6;
     double k6r[3];
-    const Trig tn = trig_lv<LV, CAREFUL>(na);
+    Trig tn = trig_lv<LV, CAREFUL>(na);
     rhs_core_lv<LV>(p, tn, nu, nR, K6.uz, K6.R);
     stage_at<false>(p, tn, nu, nR, K6, k6r);
     st.nfev += 6;
@@ -668,22 +668,39 @@ __device__ __forceinline__ void rk45_attempt_lv(const SegPar &p, double yu[3], d
     double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
     if (rejected) factor = fmin(1.0, factor);
     ha *= ok ? factor : fmax(0.2, fpow);
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        if (i < NU) yu[i] = ok ? nu[i] : yu[i];
-        if (i < NA) ya[i] = ok ? na[i] : ya[i];
-        yr[i] = ok ? nr[i] : yr[i];
+    if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+        // a lane rejects (rare: the env workload rejects ~1e-3 attempts per FK): its "new" state
+        // becomes its old one, so every lane takes the plain assignments below, which cost the
+        // allocator at most a copy where per-dword selects on the accept path cost a v_cndmask each
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            nu[i] = ok ? nu[i] : yu[i];
+            na[i] = ok ? na[i] : ya[i];
+            nr[i] = ok ? nr[i] : yr[i];
+            K6.uz[i] = ok ? K6.uz[i] : f.uz[i];
+            K6.al[i] = ok ? K6.al[i] : f.al[i];
+        }
+        #pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            nR[i] = ok ? nR[i] : yR[i];
+            K6.R[i] = ok ? K6.R[i] : f.R[i];
+        }
+        tn.c10 = ok ? tn.c10 : ty.c10; tn.s10 = ok ? tn.s10 : ty.s10;
+        tn.c20 = ok ? tn.c20 : ty.c20; tn.s20 = ok ? tn.s20 : ty.s20;
+        tn.c21 = ok ? tn.c21 : ty.c21; tn.s21 = ok ? tn.s21 : ty.s21;
+        tnew = ok ? tnew : t;
     }
     #pragma unroll
-    for (int i = 0; i < 9; ++i) yR[i] = ok ? nR[i] : yR[i];
+    for (int i = 0; i < 3; ++i) {
+        if (i < NU) yu[i] = nu[i];
+        if (i < NA) ya[i] = na[i];
+        yr[i] = nr[i];
+    }
     #pragma unroll
-    for (int i = 0; i < 3; ++i) { f.uz[i] = ok ? K6.uz[i] : f.uz[i]; f.al[i] = ok ? K6.al[i] : f.al[i]; }
-    #pragma unroll
-    for (int i = 0; i < 9; ++i) f.R[i] = ok ? K6.R[i] : f.R[i];
-    ty.c10 = ok ? tn.c10 : ty.c10; ty.s10 = ok ? tn.s10 : ty.s10;
-    ty.c20 = ok ? tn.c20 : ty.c20; ty.s20 = ok ? tn.s20 : ty.s20;
-    ty.c21 = ok ? tn.c21 : ty.c21; ty.s21 = ok ? tn.s21 : ty.s21;
-    t = ok ? tnew : t;
+    for (int i = 0; i < 9; ++i) yR[i] = nR[i];
+    f = K6;
+    ty = tn;
+    t = tnew;
     st.nstep += ok ? 1u : 0u;
     st.nrej += ok ? 0u : 1u;
     new_step = ok;
@@ -1012,7 +1029,7 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         }
         Stage K6;
         double k6r[3];
-        const Trig tn = RIGID ? ty : trig_of<CAREFUL>(na);
+        Trig tn = RIGID ? ty : trig_of<CAREFUL>(na);
         rhs_core<HAS_UY>(p, tn, nu, nR, K6.uz, K6.R);
         stage_at<false>(p, tn, nu, nR, K6, k6r);
         st.nfev += 6;
@@ -1050,22 +1067,33 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
             double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
             ha *= ok ? factor : fmax(0.2, fpow);
-            #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                yu[i] = ok ? nu[i] : yu[i];
-                ya[i] = ok ? na[i] : ya[i];
-                yr[i] = ok ? nr[i] : yr[i];
+            if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+                // a lane rejects (rare): its "new" state becomes its old one (rk45_attempt_lv)
+                #pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    nu[i] = ok ? nu[i] : yu[i];
+                    na[i] = ok ? na[i] : ya[i];
+                    nr[i] = ok ? nr[i] : yr[i];
+                    K6.uz[i] = ok ? K6.uz[i] : f.uz[i];
+                    K6.al[i] = ok ? K6.al[i] : f.al[i];
+                }
+                #pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    nR[i] = ok ? nR[i] : yR[i];
+                    K6.R[i] = ok ? K6.R[i] : f.R[i];
+                }
+                tn.c10 = ok ? tn.c10 : ty.c10; tn.s10 = ok ? tn.s10 : ty.s10;
+                tn.c20 = ok ? tn.c20 : ty.c20; tn.s20 = ok ? tn.s20 : ty.s20;
+                tn.c21 = ok ? tn.c21 : ty.c21; tn.s21 = ok ? tn.s21 : ty.s21;
+                tnew = ok ? tnew : t;
             }
             #pragma unroll
-            for (int i = 0; i < 9; ++i) yR[i] = ok ? nR[i] : yR[i];
+            for (int i = 0; i < 3; ++i) { yu[i] = nu[i]; ya[i] = na[i]; yr[i] = nr[i]; }
             #pragma unroll
-            for (int i = 0; i < 3; ++i) { f.uz[i] = ok ? K6.uz[i] : f.uz[i]; f.al[i] = ok ? K6.al[i] : f.al[i]; }
-            #pragma unroll
-            for (int i = 0; i < 9; ++i) f.R[i] = ok ? K6.R[i] : f.R[i];
-            ty.c10 = ok ? tn.c10 : ty.c10; ty.s10 = ok ? tn.s10 : ty.s10;
-            ty.c20 = ok ? tn.c20 : ty.c20; ty.s20 = ok ? tn.s20 : ty.s20;
-            ty.c21 = ok ? tn.c21 : ty.c21; ty.s21 = ok ? tn.s21 : ty.s21;
-            t = ok ? tnew : t;
+            for (int i = 0; i < 9; ++i) yR[i] = nR[i];
+            f = K6;
+            ty = tn;
+            t = tnew;
             st.nstep += ok ? 1u : 0u;
             st.nrej += ok ? 0u : 1u;
             new_step = ok;
