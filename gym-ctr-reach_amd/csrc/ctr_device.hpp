@@ -663,7 +663,7 @@ __device__ __forceinline__ void rk45_attempt_lv(const SegPar &p, double yu[3], d
     // unguarded: for en2n >= 1e300 (or inf / NaN) the root is < 2e-30 (or NaN) and only enters
     // fmax(0.2, fpow) of a rejection, which is 0.2 either way (rk.py:171)
     const double fpow = 0.9 * ctr_math::inv_root10(en2n);
-    // accept / reject as selects (fk_lane's attempt does the same)
+    // accept / reject (fk_lane's attempt does the same)
     const bool ok = en2n < 1.0;
     double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
     if (rejected) factor = fmin(1.0, factor);
@@ -1060,9 +1060,9 @@ __device__ bool fk_lane(const SysK &sy, const double q[6], double tip[3], FkStat
         const double fpow = 0.9 * ctr_math::inv_root10(en2n);
         CTR_STAMP(ts3);
         if constexpr (!SHAPE) {
-            // accept / reject (rk.py:160-175) as selects: in most iterations some lanes of a wave
-            // accept and some reject, so an if / else ran both sides, each copying the loop-carried
-            // state into the join's registers (DESIGN.md 4.5 log: -1.3 us, bit-equal)
+            // accept / reject (rk.py:160-175): every lane takes the new state by plain assignment;
+            // a rejecting lane (rare, see rk45_attempt_lv) first sets its new state to its old one
+            // inside a wave-uniform branch (DESIGN.md 4.5 log: -2.6 us, bit-equal)
             const bool ok = en2n < 1.0;
             double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
             if (rejected) factor = fmin(1.0, factor);
