@@ -317,9 +317,13 @@ __device__ __noinline__ bool gather_wait_slot(const ctr_gather_push_t *g, uint32
 __device__ __noinline__ void gather_poison_lanes(const ctr_gather_push_t *g, uint32_t seq)
 {
     const int lane = (int)(threadIdx.x & 63);
-    if (lane < g->world && !seq_reached(__hip_atomic_load(g->rel + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                                        seq - (uint32_t)g->depth))
-        __hip_atomic_store(g->poisonw[lane], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // a NULL poison word: not enabled for that consumer (a C caller that left the ABI-14 fields
+    // zeroed gets only its own err bit).  The stored marker is never 0 (0 = not poisoned), also
+    // when the step counter has wrapped to 0.
+    if (lane < g->world && g->poisonw[lane] != nullptr &&
+        !seq_reached(__hip_atomic_load(g->rel + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                     seq - (uint32_t)g->depth))
+        __hip_atomic_store(g->poisonw[lane], seq ? seq : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -333,7 +337,7 @@ __device__ __noinline__ void gather_wait_prev_lane(const ctr_gather_push_t *g, u
     if (lane >= g->world) return;
     // producer `lane` overran a slot of this rank before (its poison word): the views this rank
     // read before this launch may hold rows of a later step
-    if (__hip_atomic_load(g->poison + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+    if (g->poison != nullptr && __hip_atomic_load(g->poison + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
         atomicOr(g->err, CTR_GATHER_E_RELEASE_TIMEOUT);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -1139,14 +1143,18 @@ struct CarryHdr {
 };
 static_assert(sizeof(CarryHdr) == 1024, "CarryHdr layout");
 
-// One FK of a refill: the scipy-RK45 FK runs at most `budget` iterations (the compliant RK4 FK
-// at most `budget` RK4 steps) and can start from a suspended state (fk_lane / fk_lane_rk4
-// RESUME); the rigid model's segment maps always run to the end.
+// One FK of a refill: the scipy-RK45 FK (either model) runs at most `budget` iterations (the
+// compliant RK4 FK at most `budget` RK4 steps) and can start from a suspended state (fk_lane /
+// fk_lane_rk4 RESUME); the rigid model's fixed-step RK4 (segment maps on 8-lane groups) always
+// runs to the end.
+template <int MODE>
+constexpr bool refill_resumable() { return (MODE & 6) != 6; }
+
 template <int MODE>
 __device__ __forceinline__ bool fk_refill(const KCfg &kc, const SysK &sy, const float q[6], double tip[3], FkStats &st,
                                           const FkSuspend *from, FkSuspend *to, int budget)
 {
-    if constexpr ((MODE & 4) != 0) {
+    if constexpr (!refill_resumable<MODE>()) {
         fk_dispatch<MODE>(kc, sy, q, tip, st);
         return true;
     } else if constexpr ((MODE & 2) != 0) {
@@ -1170,7 +1178,7 @@ __device__ __forceinline__ bool fk_refill(const KCfg &kc, const SysK &sy, const 
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
 {
-    constexpr bool RESUMABLE = (MODE & 4) == 0;           // scipy RK45 and compliant RK4
+    constexpr bool RESUMABLE = refill_resumable<MODE>();  // all but the rigid model's RK4
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
     __shared__ int64_t s_count, s_carried;

@@ -184,11 +184,14 @@ class CtrReachVecEnv(object):
         # long as the budget instead of its slowest fresh sample's FK (ctr_batch_t.carry).  The
         # resets less than a period ahead always finish: none is due before it lands
         R = max(1, int(refill_interval))
-        resumable = integrator == "rk45_scipy" or model == "compliant"
+        # the kernel's rule (ctr_kernels.hip refill_resumable): every mode but the rigid model's
+        # fixed-step RK4, whose FKs run as segment maps on 8-lane groups
+        resumable = not (integrator == "rk4" and model == "rigid")
         if refill_budget is None:
             refill_budget = (6 if integrator == "rk45_scipy" else RK4_REFILL_BUDGET) if resumable else 0
         if refill_budget and not resumable:
-            raise ValueError("refill_budget needs the compliant model (the rigid model's FKs run as segment maps)")
+            raise ValueError("refill_budget is not available for the rigid model's fixed-step RK4 (its FKs run as "
+                             "segment maps)")
         if pool_depth is None:
             # deep enough for the budget to apply over about two refills (queued resets are
             # P - R - 1 or more ahead); 64 slots cap the default ring (108 B per env and slot).
@@ -476,6 +479,13 @@ class CtrReachVecEnv(object):
                                  _abi.ptr(status), _abi.stream_ptr(stream))
             _abi.check(rc, "ctr_fk")
         if return_stats:
+            if self.integrator == "rk4":
+                # ctr_fk packs stats[2] for fixed-step RK4 (include/ctr_reach_amd.h): the segments run
+                # as segment maps << 16 | their square-and-multiply compositions; RK4 rejects nothing.
+                # nstep counts the RK4 steps taken stage by stage (nfev: 4 per step, mapped or not)
+                packed = stats[:, 2]
+                return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=torch.zeros_like(packed),
+                                 maps=packed >> 16, compositions=packed & 0xFFFF, nseg=stats[:, 3], status=status)
             return tip, dict(nfev=stats[:, 0], nstep=stats[:, 1], nrej=stats[:, 2], nseg=stats[:, 3], status=status)
         return tip
 

@@ -163,8 +163,9 @@ typedef struct ctr_batch_t {
     int32_t  *refill;            /* [2 + 2 refill_cap]: count, (env, reset number) pairs,
                                     then a completion ticket (zero-initialised)          */
     int64_t   refill_cap;
-    /* Resumable refill (optional, carry NULL disables it; scipy RK45, and fixed-step RK4 on the
-     * compliant model -- the rigid model's segment maps ignore it).  A reset at least
+    /* Resumable refill (optional, carry NULL disables it; scipy RK45 on either model, and
+     * fixed-step RK4 on the compliant model -- the rigid model's RK4 segment maps ignore it).
+     * A reset at least
      * refill_lead resets ahead of its environment (r - epoch - 1 >= refill_lead at the time of
      * the refill) runs at most refill_budget iterations (segment start + RK45 attempt; one RK4
      * step) of each of its two FKs in one ctr_pool_refill; an unfinished one is suspended
@@ -475,11 +476,15 @@ struct ctr_gather_push_t {
                                                  microseconds (ABI 14; was a poll count)     */
     /* ABI 14: */
     uint32_t   *poisonw[CTR_GATHER_MAX_RANKS];/* this rank's poison word in rank p's memory: on a
-                                                 release time-out, step seq is stored into the
-                                                 words of the consumers that had not released */
+                                                 release time-out, step seq (1 if seq has
+                                                 wrapped to 0) is stored into the words of the
+                                                 consumers that had not released; a NULL entry
+                                                 = not enabled for that consumer             */
     const uint32_t *poison;                   /* [world] this rank's poison words (producer p's
                                                  at [p]; zeroed, sticky): non-zero = a producer
-                                                 overwrote a slot this rank had not released  */
+                                                 overwrote a slot this rank had not released;
+                                                 NULL = not enabled (only the producer's err
+                                                 reports an overrun then)                    */
 };
 
 /* Enqueue the push kernel: the n rows to every dst[p] (p < world), then seq to every seqw[p]

@@ -39,9 +39,38 @@ def test_fk_modes_vs_oracle(cuda, oracle_mod, integrator, spm, model):
     nfev = st["nfev"].cpu().numpy()
     if integrator == "rk4":
         np.testing.assert_array_equal(nfev, ref["nfev"])
+        # the packed stats[2] is decoded: no rejections, the mapped segments apart
+        assert (st["nrej"].cpu().numpy() == 0).all()
+        maps = st["maps"].cpu().numpy()
+        assert (maps <= st["nseg"].cpu().numpy()).all() and (st["compositions"].cpu().numpy() >= 0).all()
+        if model == "rigid":
+            assert (maps > 0).all()
     else:
         assert (nfev == ref["nfev"]).mean() > 0.999
     assert (st["status"].cpu().numpy() == 0).all()
+
+
+@pytest.mark.parametrize("name", ["fk_random.npz", "fk_edge.npz", "csv_known.npz"])
+def test_configs4_rk4_400_vs_reference_fixtures(cuda, golden_dir, name):
+    """configs[4]'s GPU FK (compliant, RK4 at 400 steps/m) straight against the REFERENCE's tips
+    (scipy RK45, model.py:141-151) on its own fixtures: the north_star bar (<= 1e-4 m) with the
+    per-system bars of test_oracle_modes.RK4_400_BARS, and p99.9 <= 1e-4 m per system."""
+    import os
+    from ctr_reach_amd import CtrReachVecEnv
+    from test_oracle_modes import RK4_400_BARS
+    d = np.load(os.path.join(golden_dir, name))
+    ref = d["tip"] if "tip" in d.files else d["tip_reference"]
+    sysid = d["system"].astype(np.int32)
+    env = CtrReachVecEnv(1, device=cuda, select_systems=[0, 1, 2, 3], integrator="rk4",
+                         rk4_steps_per_m=400, model="compliant")
+    tip = env.forward_kinematics(d["joints"].astype(np.float32), sysid).cpu().numpy()
+    err = np.linalg.norm(tip - ref, axis=1)
+    for s, bar in RK4_400_BARS.items():
+        e = err[sysid == s]
+        if e.size:
+            assert e.max() < bar, (s, e.max())
+            assert np.quantile(e, 0.999) <= 1e-4, (s, np.quantile(e, 0.999))
+    assert (err <= 1e-4).mean() >= 0.999
 
 
 @pytest.mark.parametrize("integrator,spm,model", MODES[:3])
@@ -212,6 +241,6 @@ def test_fk_is_independent_of_wave_composition(cuda, oracle_mod, integrator, spm
     tip_p, st_p = env.forward_kinematics(q[perm], sysid[perm], return_stats=True)
     inv = np.argsort(perm)
     np.testing.assert_array_equal(tip_p.cpu().numpy()[inv], tip.cpu().numpy())
-    for k in ("nfev", "nstep", "nrej", "nseg", "status"):
+    for k in st:                      # nfev nstep nrej nseg status (+ RK4's maps, compositions)
         np.testing.assert_array_equal(st_p[k].cpu().numpy()[inv], st[k].cpu().numpy(), err_msg=k)
     torch.cuda.synchronize()

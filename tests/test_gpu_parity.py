@@ -369,6 +369,13 @@ def test_rk4_reset_pool_matches_synchronous_resets(cuda, model, depth, interval,
     _pool_parity(cuda, depth, interval, rand, budget, integrator="rk4", rk4_steps_per_m=400, model=model)
 
 
+@pytest.mark.parametrize("depth,interval,rand,budget", [(None, 4, 0.0, None), (16, 3, 0.05, 2), (4, 8, 0.0, None)])
+def test_rk45_rigid_reset_pool_matches_synchronous_resets(cuda, depth, interval, rand, budget):
+    """The rigid model under scipy RK45: its refill is resumable like the compliant
+    model's (suspended RK45 FKs on the carry lists, finished bit-identically by the next refill)."""
+    _pool_parity(cuda, depth, interval, rand, budget, integrator="rk45_scipy", model="rigid")
+
+
 def _pool_parity(cuda, depth, interval, rand, budget, **solver):
     import torch
     n = 4096
@@ -376,7 +383,8 @@ def _pool_parity(cuda, depth, interval, rand, budget, **solver):
     a = _env(cuda, n, pool_depth=0, **kw)
     b = _env(cuda, n, pool_depth=depth, refill_interval=interval, refill_budget=budget, **kw)
     resumable = b.carry is not None
-    assert resumable == (b.pool_depth > 2 * interval and solver.get("model", "compliant") == "compliant")
+    rigid_rk4 = solver.get("model") == "rigid" and solver.get("integrator") == "rk4"
+    assert resumable == (b.pool_depth > 2 * interval and not rigid_rk4)
     a.goal_tolerance.current_tol = b.goal_tolerance.current_tol = 0.03   # plenty of early successes
     a.reset(); b.reset()
     rng = np.random.default_rng(4)
