@@ -536,6 +536,47 @@ struct PoolPre {
     double dg[3], ag[3];
 };
 
+// The slot's first 112 B (every field) as 7 dwordx4 loads of its one 128-B line.
+__device__ __forceinline__ void pool_load(const ctr_pool_slot_t *sl, PoolPre &pp)
+{
+    static_assert(sizeof(ctr_pool_slot_t) == 128 && offsetof(ctr_pool_slot_t, r) == 104, "ctr_pool_slot_t layout");
+    const uint4 *v = reinterpret_cast<const uint4 *>(sl);
+    uint4 w[7];
+    #pragma unroll
+    for (int k = 0; k < 7; ++k) w[k] = v[k];
+    ctr_pool_slot_t row;
+    __builtin_memcpy(&row, w, sizeof w);
+    pp.loaded = true;
+    pp.pr = row.r;
+    pp.sys = row.sys;
+    pp.stat = row.stat;
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) { pp.q0[i] = row.q0[i]; pp.qd[i] = row.qd[i]; }
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { pp.dg[i] = row.dg[i]; pp.ag[i] = row.ag[i]; }
+}
+
+// The slot as 8 dwordx4 stores (the whole line, pad zeroed): the refill's writes.
+__device__ __forceinline__ void pool_store(ctr_pool_slot_t *sl, const float qd[6], const float q0[6], const double dg[3],
+                                           const double ag[3], int32_t sys, uint32_t stat, uint32_t r)
+{
+    ctr_pool_slot_t row;
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { row.dg[i] = dg[i]; row.ag[i] = ag[i]; }
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) { row.qd[i] = qd[i]; row.q0[i] = q0[i]; }
+    row.sys = sys;
+    row.stat = stat;
+    row.r = r;
+    #pragma unroll
+    for (int i = 0; i < 5; ++i) row.pad[i] = 0u;
+    uint4 w[8];
+    __builtin_memcpy(w, &row, sizeof w);
+    uint4 *v = reinterpret_cast<uint4 *>(sl);
+    #pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = w[k];
+}
+
 // ALL: load every env's next reset, not only the time-limit ones (the rigid 8-lane group path:
 // latency-bound, with registers to spare, and its successes are as likely to sit on the slowest
 // wave's tail).
@@ -547,18 +588,7 @@ __device__ __forceinline__ void pool_prefetch(const KCfg &kc, const ctr_batch_t 
     const int P = b.pool_depth;
     if (!autoreset || P <= 0 || (!ALL && t + 1 < kc.c.max_steps)) return;
     const uint32_t r = epoch + 1;
-    const int64_t ps = (int64_t)(r % (uint32_t)P) * b.n + e;
-    pp.loaded = true;
-    pp.pr = b.pool_r[ps];
-    pp.sys = b.pool_sys[ps];
-    pp.stat = b.pool_stat[ps];
-    #pragma unroll
-    for (int i = 0; i < 6; ++i) pp.q0[i] = b.pool_q0[6 * ps + i];
-    if (b.desired_joints)
-        #pragma unroll
-        for (int i = 0; i < 6; ++i) pp.qd[i] = b.pool_qd[6 * ps + i];
-    #pragma unroll
-    for (int i = 0; i < 3; ++i) { pp.dg[i] = b.pool_dg[3 * ps + i]; pp.ag[i] = b.pool_ag[3 * ps + i]; }
+    pool_load(b.pool + ((int64_t)(r % (uint32_t)P) * b.n + e), pp);
 }
 
 struct StepFlags {
@@ -617,20 +647,21 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
             for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
         const uint32_t r = epoch + 1;                           // reset number to take
         const int P = b.pool_depth;
-        const int64_t ps = P > 0 ? (int64_t)(r % (uint32_t)P) * b.n + e : 0;
-        if (P > 0 && (pp.loaded ? pp.pr : b.pool_r[ps]) == r) {
+        PoolPre lp = pp;                                        // the slot of reset r (one line)
+        if (P > 0 && !pp.loaded) pool_load(b.pool + ((int64_t)(r % (uint32_t)P) * b.n + e), lp);
+        if (P > 0 && lp.pr == r) {
             // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
-            const int s2 = clamp_sys(pp.loaded ? pp.sys : b.pool_sys[ps], kc.c.n_systems);
+            const int s2 = clamp_sys(lp.sys, kc.c.n_systems);
             #pragma unroll
-            for (int i = 0; i < 6; ++i) q[i] = pp.loaded ? pp.q0[i] : b.pool_q0[6 * ps + i];
+            for (int i = 0; i < 6; ++i) q[i] = lp.q0[i];
             #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                dg[i] = pp.loaded ? pp.dg[i] : b.pool_dg[3 * ps + i];
-                ag[i] = pp.loaded ? pp.ag[i] : b.pool_ag[3 * ps + i];
+                dg[i] = lp.dg[i];
+                ag[i] = lp.ag[i];
             }
             if (b.desired_joints)
                 #pragma unroll
-                for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = pp.loaded ? pp.qd[i] : b.pool_qd[6 * ps + i];
+                for (int i = 0; i < 6; ++i) b.desired_joints[6 * e + i] = lp.qd[i];
             if (b.starting_joints)
                 #pragma unroll
                 for (int i = 0; i < 6; ++i) b.starting_joints[6 * e + i] = q[i];
@@ -641,7 +672,7 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
             for (int i = 0; i < 3; ++i) b.desired_goal[3 * e + i] = dg[i];
             b.system[e] = s2;
             b.epoch[e] = r;
-            stat |= pp.loaded ? pp.stat : b.pool_stat[ps];
+            stat |= lp.stat;
             obs_lane(q, dg, ag, kc.c.tol, s2, multi, kc.c.egocentric != 0, obs);
             if (her) {                                              // the next episode starts now
                 float obf[14];
@@ -1103,7 +1134,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KCfg kc, ctr_batch_t b, int mod
         } else {
             for (int j = 1; j <= b.pool_depth; ++j) {
                 const uint32_t rr = r + (uint32_t)j;
-                const bool need = queue && b.pool_r[(int64_t)(rr % (uint32_t)b.pool_depth) * b.n + ee] != rr;
+                const bool need = queue && b.pool[(int64_t)(rr % (uint32_t)b.pool_depth) * b.n + ee].r != rr;
                 const int32_t two[2] = {(int32_t)ee, (int32_t)rr};
                 wave_append(b.refill, b.refill + 1, b.refill_cap, need, two, 2);
             }
@@ -1259,21 +1290,13 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
             const uint32_t r = queued ? (uint32_t)b.refill[2 + 2 * i] : 0u;
             const int64_t ps = queued ? (int64_t)(r % (uint32_t)b.pool_depth) * b.n + e : 0;
             // only the resets the env can still take from its ring (see below)
-            const bool fresh = queued && b.pool_r[ps] != r && r - (uint32_t)b.epoch[e] - 1u < (uint32_t)b.pool_depth;
+            const bool fresh = queued && b.pool[ps].r != r && r - (uint32_t)b.epoch[e] - 1u < (uint32_t)b.pool_depth;
             // every queued entry draws and integrates (a reset is a pure function of (seed, env,
             // r): an entry that is not fresh computes what it would discard), so the pool_r /
             // epoch loads behind `fresh` overlap the sampling instead of preceding it
             const ResetOut ro = reset_pair<MODE>(kc, s_sys, s_raw, queued, odd, (uint64_t)(b.env_base + e), r, nullptr,
                                                    nullptr, -1);
-            if (fresh && RL::writer()) {
-                #pragma unroll
-                for (int k = 0; k < 6; ++k) { b.pool_qd[6 * ps + k] = ro.qd[k]; b.pool_q0[6 * ps + k] = ro.q0[k]; }
-                #pragma unroll
-                for (int k = 0; k < 3; ++k) { b.pool_dg[3 * ps + k] = ro.dg[k]; b.pool_ag[3 * ps + k] = ro.ag[k]; }
-                b.pool_sys[ps] = ro.sys;
-                b.pool_stat[ps] = ro.stat;
-                b.pool_r[ps] = r;
-            }
+            if (fresh && RL::writer()) pool_store(b.pool + ps, ro.qd, ro.q0, ro.dg, ro.ag, ro.sys, ro.stat, r);
             continue;
         }
         const bool carried = i < c;                       // pair-uniform, as everything below
@@ -1303,7 +1326,7 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         const uint32_t lead = (queued || carried) ? r - (uint32_t)b.epoch[e] - 1u : 0u;   // resets before r
         // (queued or carried alike: a suspended reset the env has passed meanwhile -- a miss sweep
         // took it -- or whose slot already holds it is dropped, not finished into a stale slot)
-        const bool fresh = (queued || carried) && b.pool_r[ps] != r && lead < (uint32_t)b.pool_depth;
+        const bool fresh = (queued || carried) && b.pool[ps].r != r && lead < (uint32_t)b.pool_depth;
         const uint64_t genv = (uint64_t)(b.env_base + e);
         // every queued entry draws (draws are a pure function of (seed, env, r); one that is not
         // fresh discards its joints), so the pool_r / epoch loads behind `fresh` overlap the
@@ -1348,15 +1371,8 @@ __global__ __launch_bounds__(BLOCK) void k_refill(KCfg kc, ctr_batch_t b)
         #pragma unroll
         for (int k = 0; k < 6; ++k) oq[k] = __shfl_xor(qv[k], 1);
         const uint32_t ofst = __shfl_xor(fst, 1);
-        if (active && fin && ofin && odd) {               // both FKs done: the pool slot
-            #pragma unroll
-            for (int k = 0; k < 6; ++k) { b.pool_qd[6 * ps + k] = oq[k]; b.pool_q0[6 * ps + k] = qv[k]; }
-            #pragma unroll
-            for (int k = 0; k < 3; ++k) { b.pool_dg[3 * ps + k] = otip[k]; b.pool_ag[3 * ps + k] = tip[k]; }
-            b.pool_sys[ps] = s;
-            b.pool_stat[ps] = stat | fst | ofst;
-            b.pool_r[ps] = r;
-        }
+        if (active && fin && ofin && odd)                 // both FKs done: the pool slot
+            pool_store(b.pool + ps, oq, qv, otip, tip, s, stat | fst | ofst, r);
         if constexpr (RESUMABLE) {
             // a pair with a suspended FK goes onto the other list (one atomic per wave)
             const bool keep = active && !(fin && ofin);
@@ -1429,7 +1445,7 @@ __global__ __launch_bounds__(BLOCK) void k_pool_requeue(ctr_batch_t b)
         uint64_t m = 0;
         for (int j = 0; j < 64 && 64 * w + j < P && in; ++j) {
             const uint32_t rr = r + 1u + (uint32_t)(64 * w + j);
-            if (b.pool_r[(int64_t)(rr % (uint32_t)P) * b.n + e] != rr) m |= 1ull << j;
+            if (b.pool[(int64_t)(rr % (uint32_t)P) * b.n + e].r != rr) m |= 1ull << j;
         }
         miss[w] = m;
     }
@@ -1510,9 +1526,10 @@ int check_batch(const ctr_batch_t &b, const char *who)
         return fail(CTR_EINVAL, who);
     if (b.pool_depth < 0 || b.pool_depth > CTR_POOL_MAX)
         return fail(CTR_EINVAL, "pool_depth out of range (0..CTR_POOL_MAX = 192)");
-    if (b.pool_depth > 0 && (!b.pool_qd || !b.pool_dg || !b.pool_q0 || !b.pool_ag || !b.pool_sys || !b.pool_r ||
-                             !b.pool_stat || !b.refill || b.refill_cap <= 0))
-        return fail(CTR_EINVAL, "pool_depth > 0 needs every pool buffer and a refill queue");
+    if (b.pool_depth > 0 && (!b.pool || !b.refill || b.refill_cap <= 0))
+        return fail(CTR_EINVAL, "pool_depth > 0 needs the pool and a refill queue");
+    if (b.pool_depth > 0 && ((uintptr_t)b.pool & 127u) != 0)
+        return fail(CTR_EINVAL, "the reset pool must be 128-B aligned (one cache line per slot)");
     if (b.carry && (b.carry_cap <= 0 || b.carry_cap > 0x3fffffff || b.refill_budget < 0 || b.refill_lead < 0))
         return fail(CTR_EINVAL, "carry needs carry_cap in 1..2^30 and refill_budget, refill_lead >= 0");
     return 0;

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_REACH_AMD_LIB") or os.path.join(HERE, "lib", "libctr_reach_amd.so")
 
-CTR_ABI_VERSION = 14
+CTR_ABI_VERSION = 15
 CTR_IPC_HANDLE_BYTES = 64
 CTR_GATHER_MAX_RANKS = 16
 CTR_MAX_SYSTEMS = 8
@@ -83,13 +83,7 @@ class CtrBatch(ctypes.Structure):
         ("work_pad", ctypes.c_int32),
         ("pool_depth", ctypes.c_int32),
         ("pool_pad", ctypes.c_int32),
-        ("pool_qd", _P),
-        ("pool_dg", _P),
-        ("pool_q0", _P),
-        ("pool_ag", _P),
-        ("pool_sys", _P),
-        ("pool_r", _P),
-        ("pool_stat", _P),
+        ("pool", _P),             # [P][n] ctr_pool_slot_t, 128 B each (ABI 15)
         ("refill", _P),
         ("refill_cap", ctypes.c_int64),
         ("carry", ctypes.c_void_p),
@@ -97,6 +91,25 @@ class CtrBatch(ctypes.Structure):
         ("refill_budget", ctypes.c_int32),
         ("refill_lead", ctypes.c_int32),
     ]
+
+
+class CtrPoolSlot(ctypes.Structure):
+    """ctr_pool_slot_t: one precomputed reset, 128 B (ABI 15)."""
+    _fields_ = [("dg", ctypes.c_double * 3), ("ag", ctypes.c_double * 3), ("qd", ctypes.c_float * 6),
+                ("q0", ctypes.c_float * 6), ("sys", ctypes.c_int32), ("stat", ctypes.c_uint32),
+                ("r", ctypes.c_uint32), ("pad", ctypes.c_uint32 * 5)]
+
+
+# the slot in dwords: [first, last) dword and dtype of every field (the host's strided views)
+POOL_SLOT_DWORDS = ctypes.sizeof(CtrPoolSlot) // 4
+POOL_SLOT_FIELDS = {
+    name: (getattr(CtrPoolSlot, name).offset // 4,
+           None if getattr(CtrPoolSlot, name).size == 4 else (getattr(CtrPoolSlot, name).offset +
+                                                              getattr(CtrPoolSlot, name).size) // 4,
+           kind)
+    for name, kind in (("dg", "f64"), ("ag", "f64"), ("qd", "f32"), ("q0", "f32"), ("sys", "i32"), ("stat", "i32"),
+                       ("r", "i32"))}
+assert POOL_SLOT_DWORDS == 32
 
 
 class CtrStepOut(ctypes.Structure):

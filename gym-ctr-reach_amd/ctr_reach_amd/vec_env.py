@@ -176,7 +176,7 @@ class CtrReachVecEnv(object):
         # reset pool: resets are a pure function of (seed, env id, reset number), so they are
         # precomputed in batches every `refill_interval` steps and consumed by a copy
         # depth >= the refill interval: every env then finds its next reset in the pool on every
-        # step (CTR_AUTORESET_POOLED, no miss-sweep launch); 108 B per env and slot
+        # step (CTR_AUTORESET_POOLED, no miss-sweep launch); 128 B per env and slot
         # resumable refill (scipy RK45, and fixed-step RK4 on the compliant model): a reset at least
         # one refill period ahead of its env runs at most refill_budget iterations (RK45 attempts,
         # RK4 steps) of each FK per refill; an unfinished one is
@@ -194,7 +194,7 @@ class CtrReachVecEnv(object):
                              "segment maps)")
         if pool_depth is None:
             # deep enough for the budget to apply over about two refills (queued resets are
-            # P - R - 1 or more ahead); 64 slots cap the default ring (108 B per env and slot).
+            # P - R - 1 or more ahead); 64 slots cap the default ring (128 B per env and slot).
             # Deeper rings (up to CTR_POOL_MAX) work but measured slower: at R = 64 a 152-slot
             # ring with the budget ran the 128-step window at 78.4 against 78.0 us/step
             want = 2 * R + 24 if refill_budget else R
@@ -212,17 +212,19 @@ class CtrReachVecEnv(object):
         self._pool_full = False
         P = self.pool_depth
         if P:
-            self.pool_qd = torch.zeros((P, n, 6), dtype=f32, device=dev)
-            self.pool_dg = torch.zeros((P, n, 3), dtype=f64, device=dev)
-            self.pool_q0 = torch.zeros((P, n, 6), dtype=f32, device=dev)
-            self.pool_ag = torch.zeros((P, n, 3), dtype=f64, device=dev)
-            self.pool_sys = torch.zeros((P, n), dtype=i32, device=dev)
-            self.pool_r = torch.zeros((P, n), dtype=i32, device=dev)
-            self.pool_stat = torch.zeros((P, n), dtype=i32, device=dev)
+            # [P][n] 128-B slots (ctr_pool_slot_t): a pooled reset reads one cache line.  The
+            # per-field names are strided views of it (pool_r [P, n], pool_dg [P, n, 3], ...)
+            self.pool = torch.zeros((P, n, _abi.POOL_SLOT_DWORDS), dtype=i32, device=dev)
+            if self.pool.data_ptr() % 128:
+                raise RuntimeError("reset pool not 128-B aligned")
+            dt = {"f64": f64, "f32": f32}
+            for k, (a, b_, kind) in _abi.POOL_SLOT_FIELDS.items():
+                v = self.pool[..., a] if b_ is None else self.pool[..., a:b_].view(dt[kind])
+                setattr(self, "pool_" + k, v)
             self.refill_cap = n * (P + self.refill_interval)
             self.refill = torch.zeros(2 + 2 * self.refill_cap, dtype=i32, device=dev)   # count, pairs, ticket
         else:
-            self.pool_qd = self.pool_dg = self.pool_q0 = self.pool_ag = None
+            self.pool = self.pool_qd = self.pool_dg = self.pool_q0 = self.pool_ag = None
             self.pool_sys = self.pool_r = self.pool_stat = self.refill = None
             self.refill_cap = 0
         self.carry, self.carry_cap = None, 0
@@ -247,8 +249,7 @@ class CtrReachVecEnv(object):
         b.desired_joints, b.starting_joints = p(self.desired_joints), p(self.starting_joints)
         b.starting_position = p(self.starting_position)
         b.pool_depth = self.pool_depth
-        b.pool_qd, b.pool_dg, b.pool_q0, b.pool_ag = p(self.pool_qd), p(self.pool_dg), p(self.pool_q0), p(self.pool_ag)
-        b.pool_sys, b.pool_r, b.pool_stat = p(self.pool_sys), p(self.pool_r), p(self.pool_stat)
+        b.pool = p(self.pool)
         b.refill, b.refill_cap = p(self.refill), self.refill_cap
         b.carry, b.carry_cap = p(self.carry), self.carry_cap
         b.refill_budget, b.refill_lead = self.refill_budget, self.refill_lead

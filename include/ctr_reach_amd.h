@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CTR_ABI_VERSION 14
+#define CTR_ABI_VERSION 15
 #define CTR_MAX_SYSTEMS 8
 #define CTR_POOL_MAX 192          /* ctr_batch_t.pool_depth limit (reset slots per environment) */
 #define CTR_EINVAL (-1)
@@ -131,6 +131,19 @@ typedef struct ctr_env_config_t {
 } ctr_env_config_t;
 
 /* Device-resident batch state, row-major per environment ([n][k]). */
+/* One precomputed reset of the pool (ABI 15): 128 B, one cache line when the pool is 128-B
+ * aligned, so a pooled auto-reset reads one line (the ABI-14 [P][n][k] arrays spread it over 7). */
+typedef struct ctr_pool_slot_t {
+    double   dg[3];              /* desired goal                   bytes   0 -  23 */
+    double   ag[3];              /* start position (its FK tip)            24 -  47 */
+    float    qd[6];              /* desired joints                         48 -  71 */
+    float    q0[6];              /* start joints                           72 -  95 */
+    int32_t  sys;                /* system index                           96      */
+    uint32_t stat;               /* CTR_STATUS_* of the precomputation    100      */
+    uint32_t r;                  /* reset number held (0 = empty)         104      */
+    uint32_t pad[5];             /*                                       108 - 127 */
+} ctr_pool_slot_t;
+
 typedef struct ctr_batch_t {
     int64_t   n;                 /* environments in this shard                        */
     int64_t   env_base;          /* global id of environment 0 (RNG key; sharding)    */
@@ -148,18 +161,13 @@ typedef struct ctr_batch_t {
     int32_t   work_pad;
     /* Reset pool (optional, pool_depth 0 disables it).  Resets are a deterministic function of
      * (seed, global env id, reset number), so they can be computed ahead of time: slot (r mod P)
-     * of env e holds reset number r (pool_r), precomputed by ctr_pool_refill; an auto-reset
-     * consumes it with a copy instead of two forward-kinematics solves.  A missing slot falls
-     * back to computing the reset in the same ctr_step call.  Layout [P][n][k]. */
+     * of env e holds reset number r (ctr_pool_slot_t.r), precomputed by ctr_pool_refill; an
+     * auto-reset consumes it with a copy instead of two forward-kinematics solves.  A missing
+     * slot falls back to computing the reset in the same ctr_step call.  Layout [P][n] of
+     * 128-B slots (ABI 15; one cache line per reset, was [P][n][k] per field). */
     int32_t   pool_depth;        /* P (0 = no pool, at most CTR_POOL_MAX)             */
     int32_t   pool_pad;
-    float    *pool_qd;           /* [P][n][6] desired joints                          */
-    double   *pool_dg;           /* [P][n][3] desired goal                            */
-    float    *pool_q0;           /* [P][n][6] start joints                            */
-    double   *pool_ag;           /* [P][n][3] start position                          */
-    int32_t  *pool_sys;          /* [P][n]    system index                            */
-    uint32_t *pool_r;            /* [P][n]    reset number held (0 = empty)           */
-    uint32_t *pool_stat;         /* [P][n]    CTR_STATUS_* of the precomputation      */
+    ctr_pool_slot_t *pool;       /* [P][n] slots, 128-B aligned, zero-initialised     */
     int32_t  *refill;            /* [2 + 2 refill_cap]: count, (env, reset number) pairs,
                                     then a completion ticket (zero-initialised)          */
     int64_t   refill_cap;

@@ -83,6 +83,15 @@ def test_autoreset_modes_and_pool_requeue_validate_without_gpu():
     assert lib.ctr_step_her(cfg, b, fake, o, _abi.AUTORESET_SWEEP, h, None) == -1
     assert b"env_base" in lib.ctr_last_error()
     assert lib.ctr_pool_requeue(cfg, None, None) == -1
+    # ABI 15: the pool is one array of 128-B slots, which must be line-aligned
+    b.pool_depth, b.refill, b.refill_cap = 4, fake, 64
+    b.pool = ctypes.c_void_p(16 + 64)
+    assert lib.ctr_pool_refill(cfg, b, None) == -1
+    assert b"128-B aligned" in lib.ctr_last_error()
+    b.pool = None
+    assert lib.ctr_pool_refill(cfg, b, None) == -1
+    assert b"needs the pool" in lib.ctr_last_error()
+    b.pool_depth = 0
     b.n = 0
     assert lib.ctr_pool_requeue(cfg, b, None) == 0                     # empty batch: no-op
 
@@ -93,7 +102,8 @@ def test_struct_layout_matches_header(tmp_path):
     structs = [(_abi.CtrSystem, "ctr_system_t"), (_abi.CtrTubeRaw, "ctr_tube_raw_t"),
                (_abi.CtrEnvConfig, "ctr_env_config_t"), (_abi.CtrBatch, "ctr_batch_t"),
                (_abi.CtrStepOut, "ctr_step_out_t"), (_abi.CtrHer, "ctr_her_t"), (_abi.CtrHerBatch, "ctr_her_batch_t"),
-               (_abi.CtrCopy, "ctr_copy_t"), (_abi.CtrGatherPush, "ctr_gather_push_t")]
+               (_abi.CtrCopy, "ctr_copy_t"), (_abi.CtrGatherPush, "ctr_gather_push_t"),
+               (_abi.CtrPoolSlot, "ctr_pool_slot_t")]
     lines, want = [], []
     for cls, cname in structs:
         lines.append('  printf("%%zu\\n", sizeof(%s));' % cname)
