@@ -536,45 +536,55 @@ struct PoolPre {
     double dg[3], ag[3];
 };
 
-// The slot's first 112 B (every field) as 7 dwordx4 loads of its one 128-B line.
+// The slot's first 112 B (every field) as 7 dwordx4 loads of its one 128-B line.  The fields are
+// rebuilt from the dwords by constant index (no aggregate copy: that went through scratch).
 __device__ __forceinline__ void pool_load(const ctr_pool_slot_t *sl, PoolPre &pp)
 {
-    static_assert(sizeof(ctr_pool_slot_t) == 128 && offsetof(ctr_pool_slot_t, r) == 104, "ctr_pool_slot_t layout");
+    static_assert(sizeof(ctr_pool_slot_t) == 128 && offsetof(ctr_pool_slot_t, ag) == 24 &&
+                  offsetof(ctr_pool_slot_t, qd) == 48 && offsetof(ctr_pool_slot_t, q0) == 72 &&
+                  offsetof(ctr_pool_slot_t, sys) == 96 && offsetof(ctr_pool_slot_t, r) == 104, "ctr_pool_slot_t layout");
     const uint4 *v = reinterpret_cast<const uint4 *>(sl);
-    uint4 w[7];
+    uint32_t d[28];
     #pragma unroll
-    for (int k = 0; k < 7; ++k) w[k] = v[k];
-    ctr_pool_slot_t row;
-    __builtin_memcpy(&row, w, sizeof w);
+    for (int k = 0; k < 7; ++k) {
+        const uint4 w = v[k];
+        d[4 * k] = w.x; d[4 * k + 1] = w.y; d[4 * k + 2] = w.z; d[4 * k + 3] = w.w;
+    }
     pp.loaded = true;
-    pp.pr = row.r;
-    pp.sys = row.sys;
-    pp.stat = row.stat;
     #pragma unroll
-    for (int i = 0; i < 6; ++i) { pp.q0[i] = row.q0[i]; pp.qd[i] = row.qd[i]; }
+    for (int i = 0; i < 3; ++i) {
+        pp.dg[i] = __hiloint2double((int)d[2 * i + 1], (int)d[2 * i]);
+        pp.ag[i] = __hiloint2double((int)d[6 + 2 * i + 1], (int)d[6 + 2 * i]);
+    }
     #pragma unroll
-    for (int i = 0; i < 3; ++i) { pp.dg[i] = row.dg[i]; pp.ag[i] = row.ag[i]; }
+    for (int i = 0; i < 6; ++i) { pp.qd[i] = __uint_as_float(d[12 + i]); pp.q0[i] = __uint_as_float(d[18 + i]); }
+    pp.sys = (int32_t)d[24];
+    pp.stat = d[25];
+    pp.pr = d[26];
 }
 
 // The slot as 8 dwordx4 stores (the whole line, pad zeroed): the refill's writes.
 __device__ __forceinline__ void pool_store(ctr_pool_slot_t *sl, const float qd[6], const float q0[6], const double dg[3],
                                            const double ag[3], int32_t sys, uint32_t stat, uint32_t r)
 {
-    ctr_pool_slot_t row;
+    uint32_t d[32];
     #pragma unroll
-    for (int i = 0; i < 3; ++i) { row.dg[i] = dg[i]; row.ag[i] = ag[i]; }
+    for (int i = 0; i < 3; ++i) {
+        d[2 * i] = (uint32_t)__double2loint(dg[i]);
+        d[2 * i + 1] = (uint32_t)__double2hiint(dg[i]);
+        d[6 + 2 * i] = (uint32_t)__double2loint(ag[i]);
+        d[6 + 2 * i + 1] = (uint32_t)__double2hiint(ag[i]);
+    }
     #pragma unroll
-    for (int i = 0; i < 6; ++i) { row.qd[i] = qd[i]; row.q0[i] = q0[i]; }
-    row.sys = sys;
-    row.stat = stat;
-    row.r = r;
+    for (int i = 0; i < 6; ++i) { d[12 + i] = __float_as_uint(qd[i]); d[18 + i] = __float_as_uint(q0[i]); }
+    d[24] = (uint32_t)sys;
+    d[25] = stat;
+    d[26] = r;
     #pragma unroll
-    for (int i = 0; i < 5; ++i) row.pad[i] = 0u;
-    uint4 w[8];
-    __builtin_memcpy(w, &row, sizeof w);
+    for (int i = 27; i < 32; ++i) d[i] = 0u;
     uint4 *v = reinterpret_cast<uint4 *>(sl);
     #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = w[k];
+    for (int k = 0; k < 8; ++k) v[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
 }
 
 // ALL: load every env's next reset, not only the time-limit ones (the rigid 8-lane group path:
@@ -602,7 +612,7 @@ struct StepFlags {
 __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o, int64_t e,
                                             int s, float q[6], double ag[3], const FkStats &st, int32_t autoreset,
                                             StepFlags &fl, const ctr_her_t *her, const float *action,
-                                            const PoolPre &pp, int32_t t_prev, uint32_t epoch, const double dg_prev[3],
+                                            PoolPre &lp, int32_t t_prev, uint32_t epoch, const double dg_prev[3],
                                             float4 &grow)
 {
     const int32_t t = t_prev + 1;
@@ -647,8 +657,8 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
             for (int i = 0; i < 3; ++i) o.terminal_achieved[3 * e + i] = ag[i];
         const uint32_t r = epoch + 1;                           // reset number to take
         const int P = b.pool_depth;
-        PoolPre lp = pp;                                        // the slot of reset r (one line)
-        if (P > 0 && !pp.loaded) pool_load(b.pool + ((int64_t)(r % (uint32_t)P) * b.n + e), lp);
+        // the slot of reset r (one line), unless the step's start prefetched it
+        if (P > 0 && !lp.loaded) pool_load(b.pool + ((int64_t)(r % (uint32_t)P) * b.n + e), lp);
         if (P > 0 && lp.pr == r) {
             // pooled reset: the precomputed draws + FKs of reset r (ctr_reach_env.py:70-114)
             const int s2 = clamp_sys(lp.sys, kc.c.n_systems);

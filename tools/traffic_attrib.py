@@ -15,8 +15,8 @@ grid size and dispatch order in the counter CSV:
 usage (GPU box):  rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/tra_fetch -o run -- \\
                       python3 tools/traffic_attrib.py run
                   (and WRITE_SIZE into gpurun_out/tra_write)
-here:             python tools/traffic_attrib.py summarize gpurun_out/tra_fetch gpurun_out/tra_write
-                  -> profiles/r05_traffic_attribution.json
+here:             python tools/traffic_attrib.py summarize gpurun_out/tra_fetch gpurun_out/tra_write [tag]
+                  -> profiles/<tag>_traffic_attribution.json (default tag r06)
 """
 import csv
 import json
@@ -74,10 +74,13 @@ def run():
             while env._steps_since_refill:
                 env.step_raw(acts[0])
             phases.append(("pooled_65536", n, 3 * env.refill_interval))
+            ep0 = int(env.epoch.to(torch.int64).sum().item())
             for i in range(3 * env.refill_interval):
                 env.step_raw(acts[i % 8])
             torch.cuda.synchronize()
-    print(json.dumps({"phases": phases, "launches_per_phase": LAUNCHES}), flush=True)
+            pooled_resets = (int(env.epoch.to(torch.int64).sum().item()) - ep0) / (3 * env.refill_interval)
+    print(json.dumps({"phases": phases, "launches_per_phase": LAUNCHES,
+                      "pooled_resets_per_step": pooled_resets}), flush=True)
 
 
 def _rows(d, counter):
@@ -112,7 +115,7 @@ def split(rows):
     return {k: sum(v) / len(v) for k, v in res.items() if v}
 
 
-def summarize(fetch_dir, write_dir, factor_read=None, factor_write=1.0):
+def summarize(fetch_dir, write_dir, tag="r06", factor_read=None, factor_write=1.0):
     cal = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
     rf = factor_read or cal["read_factor"]
     fr = split(_rows(fetch_dir, "FETCH_SIZE"))
@@ -137,7 +140,13 @@ def summarize(fetch_dir, write_dir, factor_read=None, factor_write=1.0):
         "back_to_back_vs_cold_l2": {"off_65536": f64k, "cold_65536": rf * fr.get("cold_65536", 0.0)},
         "pooled_minus_off": rf * fr.get("pooled_65536", 0.0) - f64k,
     }
-    resets = RESETS_PER_STEP
+    resets, src = RESETS_PER_STEP, "bench.py headline window, resets_in_window / steps (gpurun_out/bench_r5a.log)"
+    try:                                 # the phase's own count (run() prints it into the pass's log)
+        for line in open(fetch_dir.rstrip("/") + ".log"):
+            if line.startswith("{") and "pooled_resets_per_step" in line:
+                resets, src = json.loads(line)["pooled_resets_per_step"], "counted in the pooled phase (run())"
+    except OSError:
+        pass
     pooled = rf * fr.get("pooled_65536", 0.0)
     out["named_read_excess_pooled_65536"] = {
         "total_read": pooled,
@@ -148,13 +157,14 @@ def summarize(fetch_dir, write_dir, factor_read=None, factor_write=1.0):
         "flush between launches changes nothing, so nothing of it survives a launch boundary)": fixed_64k,
         "reset_rows_as_fetched (pooled - off)": out["pooled_minus_off"],
         "bytes_per_reset_as_fetched": out["pooled_minus_off"] / resets,
-        "why_reset_rows_cost_more": "a reset reads its row from 7 SoA pool fields ([P][n][k]: r, sys, stat, q0, "
-                                    "qd, dg, ag), each a partial line of a scattered env",
+        "pool_layout": "ABI 15: one 128-B ctr_pool_slot_t per reset (a reset reads 7 dwordx4 of one line; "
+                       "round 5's [P][n][k] SoA fields spread a reset over 7 partial lines: 1 202 B fetched per "
+                       "108-B row, profiles/r05_traffic_attribution.json)",
         "resets_per_step": resets,
-        "resets_source": "bench.py headline window, resets_in_window / steps (gpurun_out/bench_r5a.log)",
+        "resets_source": src,
         "unexplained": pooled - READ_ALG * 65536 - fixed_64k - out["pooled_minus_off"],
     }
-    p = os.path.join(ROOT, "profiles", "r05_traffic_attribution.json")
+    p = os.path.join(ROOT, "profiles", "%s_traffic_attribution.json" % tag)
     with open(p, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
@@ -164,4 +174,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
     else:
-        summarize(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+        summarize(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None, sys.argv[4] if len(sys.argv) > 4 else "r06")
