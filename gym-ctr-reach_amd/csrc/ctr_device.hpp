@@ -64,14 +64,16 @@ __device__ __forceinline__ void cswap(double &a, double &b, int &ia, int &ib)
     a = ta; b = tb; ia = ja; ib = jb;
 }
 
-template <int STRIDE = CTR_BLOCK>      // LDS column stride of end_lds (lanes of the workgroup)
+// COLSHIFT: the LDS column is threadIdx.x >> COLSHIFT (1: the two lanes of an env pair share one
+// column and store the same values into it, fk_pair_rk4).
+template <int STRIDE = CTR_BLOCK, int COLSHIFT = 0>   // LDS column stride of end_lds (lanes of the workgroup)
 __device__ __forceinline__ Seg seg_build(const ctr_system_t &sy, const double beta[3], double *end_lds)
 {
 #pragma clang fp contract(off)
     // per-lane LDS column: the sorted position of each point (argsort), so the runtime-indexed
     // lookups below are one LDS read instead of a 10-way select chain; zero-length gaps as a mask
     __shared__ uint8_t s_pos[10][STRIDE];
-    const int col = threadIdx.x % STRIDE;
+    const int col = (int)(threadIdx.x >> COLSHIFT) % STRIDE;
     double v[10];
     int id[10];
     v[0] = 0.0;
@@ -1665,6 +1667,238 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
     st.nstep += (uint32_t)nsteps;
     st.nseg += (uint32_t)__builtin_popcount(sg.kept);
     if (any_long) st.status |= CTR_STATUS_TOO_LONG;
+    if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fixed-step RK4 of the compliant model (no y pre-curvature) with one env on an adjacent lane PAIR
+// (k_step for BASELINE configs[4], 512-lane workgroups).  Both lanes run one
+// instruction stream on different state slots:
+//   lane 0: A = R row 0, B = R row 1, rA = r_0, rB = r_1
+//   lane 1: A = R row 2,              rA = r_2                 (B, rB idle, kept at 0)
+// and each lane carries the whole twist (u_z, alpha) with tubes 1 and 2 in its own order: slot 1 is
+// tube "a" (lane 0: tube 1, lane 1: tube 2), slot 2 tube "b" (the other).  Per RHS each lane then
+// evaluates ONE table sincos, of alpha_a - alpha_0 (x = V[1] - V[0] on both lanes: no select), and
+// receives the other from its partner (one quad_perm DPP swap); the twist derivatives are written in
+// (a, b) form with per-lane constants (wx_a, wx_b, g_a, g_b), and the frame rows use the lane's own
+// u = (u_x,0, u_y,0, u_z,0).  The stage combinations and the update run on 12 slots + 2 r instead of
+// 18 values, the RHS on one sincos and two rows instead of two and three.  The two lanes' twists
+// are the reference ODE's, rounded in different orders (rounding-level apart from fk_lane_rk4's
+// one-lane arithmetic and from each other).
+// ------------------------------------------------------------------------------------------
+// quad_perm DPP on a 64-bit value: lane i of each quad reads lane P[i] (one v_mov_dpp per dword)
+template <int CTRL>
+__device__ __forceinline__ double dpp_qp(double x)
+{
+    const long long v = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(v & 0xffffffffll), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int DPP_FROM_ODD = 0xF5;     // quad_perm [1, 1, 3, 3]: both lanes of a pair read the odd one
+constexpr int DPP_FROM_EVEN = 0xA0;    // quad_perm [0, 0, 2, 2]
+constexpr int DPP_SWAP = 0xB1;         // quad_perm [1, 0, 3, 2]
+
+// A segment's RHS constants in the lane's tube order (SegPar, seg_fold_inv'ed: wx = inv EI Ux).
+struct PairPar {
+    double wx0, wx1, wxa, wxb, g0, g1, ga, gb;
+    bool m0, ma, mb;        // alpha' masks (tube present) of slots 0, 1, 2
+};
+
+__device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd)
+{
+    PairPar q;
+    q.wx0 = p.wx[0];
+    q.wx1 = p.wx[1];
+    q.wxa = odd ? p.wx[2] : p.wx[1];
+    q.wxb = odd ? p.wx[1] : p.wx[2];
+    q.g0 = p.g[0];
+    q.g1 = p.g[1];
+    q.ga = odd ? p.g[2] : p.g[1];
+    q.gb = odd ? p.g[1] : p.g[2];
+    q.m0 = (p.present & 1u) != 0u;
+    q.ma = ((p.present >> (odd ? 2 : 1)) & 1u) != 0u;
+    q.mb = ((p.present >> (odd ? 1 : 2)) & 1u) != 0u;
+    return q;
+}
+
+// The pair's derivative at stage input (A, B, U, V): dA, dB (rows of R [u]x), dU (du_z), dV
+// (alpha', presence-masked u_z), in the lane's tube order; r' = (A[2], B[2]) is read by the caller.
+// Level 2 (tube 2 absent): sin/cos(alpha_1 - alpha_0) only, formed from the even lane's difference
+// (the odd lane holds tube 1 in slot 2), with the same per-lane (a, b) constants (g of tube 2 = 0).
+template <int LV, bool CAREFUL>
+__device__ __forceinline__ void rhs_pair(const PairPar &p, const double A[3], const double B[3], const double U[3],
+                                         const double V[3], double dA[3], double dB[3], double dU[3], double dV[3])
+{
+    double a, b;
+    if constexpr (LV == 3) {
+        const double x = V[1] - V[0];                  // alpha_a - alpha_0
+        double sa, ca;
+        ctr_math::sincos_tab(x, s_trig_tab, sa, ca);
+        if (CAREFUL && __builtin_expect(__ballot(ctr_math::sincos_needs_slow(x)) != 0, 0) &&
+            ctr_math::sincos_needs_slow(x)) {
+            const ctr_math::SinCos r = ctr_math::sincos_slow(x);
+            sa = r.s;
+            ca = r.c;
+        }
+        const double sb = dpp_qp<DPP_SWAP>(sa), cb = dpp_qp<DPP_SWAP>(ca);   // alpha_b - alpha_0
+        const double sab = sa * cb - ca * sb;          // sin(alpha_a - alpha_b)
+        const double sy1 = fma(p.wxb, sb, p.wxa * sa); // u_y,0 (wx_1 s10 + wx_2 s20)
+        dU[0] = -(p.g0 * sy1);
+        dU[1] = p.ga * fma(p.wxb, sab, p.wx0 * sa);
+        dU[2] = p.gb * fma(-p.wxa, sab, p.wx0 * sb);
+        a = fma(p.wxb, cb, fma(p.wxa, ca, p.wx0));
+        b = sy1;
+    } else {
+        const double x = dpp_qp<DPP_FROM_EVEN>(V[1] - V[0]);   // alpha_1 - alpha_0 (the even lane's)
+        double s1, c1;
+        ctr_math::sincos_tab(x, s_trig_tab, s1, c1);
+        if (CAREFUL && __builtin_expect(__ballot(ctr_math::sincos_needs_slow(x)) != 0, 0) &&
+            ctr_math::sincos_needs_slow(x)) {
+            const ctr_math::SinCos r = ctr_math::sincos_slow(x);
+            s1 = r.s;
+            c1 = r.c;
+        }
+        const double sy1 = p.wx1 * s1;                 // rhs_core_lv<2>
+        const double sy2 = -(p.wx0 * s1);
+        dU[0] = -(p.g0 * sy1);
+        dU[1] = -(p.ga * sy2);                          // tube 1 on the even lane, tube 2 (g = 0) on the odd
+        dU[2] = -(p.gb * sy2);
+        a = fma(p.wx1, c1, p.wx0);
+        b = sy1;
+    }
+    const double u0 = U[0];
+    #pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const double *X = r ? B : A;
+        double *dX = r ? dB : dA;
+        const double r0 = X[0], r1 = X[1], r2 = X[2];
+        dX[0] = r1 * u0 - r2 * b;
+        dX[1] = r2 * a - r0 * u0;
+        dX[2] = r0 * b - r1 * a;
+    }
+    dV[0] = p.m0 ? U[0] : 0.0;                         // stage_at (masked)
+    dV[1] = p.ma ? U[1] : 0.0;
+    dV[2] = p.mb ? U[2] : 0.0;
+}
+
+// One classical RK4 step of the pair (rk4_step's combinations; a tube's zero derivatives keep its
+// slots exactly, so level 2 runs every slot).
+template <int LV, bool CAREFUL>
+__device__ __forceinline__ void rk4_step_pair(const PairPar &p, double h, double A[3], double B[3], double U[3],
+                                              double V[3], double &rA, double &rB)
+{
+    double kA[4][3], kB[4][3], kU[4][3], kV[4][3], qA[4], qB[4];
+    double iA[3], iB[3], iU[3], iV[3];
+    rhs_pair<LV, CAREFUL>(p, A, B, U, V, kA[0], kB[0], kU[0], kV[0]);
+    qA[0] = A[2];
+    qB[0] = B[2];
+    const double h2 = 0.5 * h;
+    #pragma unroll
+    for (int st = 1; st < 4; ++st) {
+        const double C = st < 3 ? h2 : h;
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            iU[i] = fma(kU[st - 1][i], C, U[i]);
+            iV[i] = fma(kV[st - 1][i], C, V[i]);
+            iA[i] = fma(kA[st - 1][i], C, A[i]);
+            iB[i] = fma(kB[st - 1][i], C, B[i]);
+        }
+        rhs_pair<LV, CAREFUL>(p, iA, iB, iU, iV, kA[st], kB[st], kU[st], kV[st]);
+        qA[st] = iA[2];
+        qB[st] = iB[2];
+    }
+    const double h6 = h * (1.0 / 6.0);
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        U[i] = fma(h6, kU[0][i] + 2.0 * (kU[1][i] + kU[2][i]) + kU[3][i], U[i]);
+        V[i] = fma(h6, kV[0][i] + 2.0 * (kV[1][i] + kV[2][i]) + kV[3][i], V[i]);
+        A[i] = fma(h6, kA[0][i] + 2.0 * (kA[1][i] + kA[2][i]) + kA[3][i], A[i]);
+        B[i] = fma(h6, kB[0][i] + 2.0 * (kB[1][i] + kB[2][i]) + kB[3][i], B[i]);
+    }
+    rA = fma(h6, qA[0] + 2.0 * (qA[1] + qA[2]) + qA[3], rA);
+    rB = fma(h6, qB[0] + 2.0 * (qB[1] + qB[2]) + qB[3], rB);
+}
+
+// fk_lane_rk4<false, false, CAREFUL> on a lane pair (see above).  Both lanes of every pair of the
+// wave must call it (in lock-step: the pair shares its segmentation and plan, one LDS column per
+// pair); the tip and the counters are returned on both lanes.
+template <bool CAREFUL>
+__device__ void fk_pair_rk4(const SysK &sy, const double q[6], bool odd, double tip[3], FkStats &st, double steps_per_m)
+{
+    const double beta[3] = {q[0], q[1], q[2]};
+    const int col = (int)(threadIdx.x >> 1);
+    double *end_lds = &s_seg_end[0][col];
+    int *n_lds = &s_seg_n[0][col];
+    const Seg sg = seg_build<CTR_BLOCK, 1>(sy, beta, end_lds);
+    const Rk4Plan pl = rk4_plan<true, false>(sg, end_lds, n_lds, steps_per_m);
+    st.nseg += (uint32_t)__builtin_popcount(sg.kept);
+    double s0, c0;
+    sincos_lds(q[3], s0, c0);
+    // R0 = Rz(alpha_0): rows (c0, -s0, 0), (s0, c0, 0), (0, 0, 1)
+    double A[3], B[3], U[3], V[3];
+    A[0] = odd ? 0.0 : c0;  A[1] = odd ? 0.0 : -s0;  A[2] = odd ? 1.0 : 0.0;
+    B[0] = odd ? 0.0 : s0;  B[1] = odd ? 0.0 : c0;   B[2] = 0.0;
+    U[0] = U[1] = U[2] = 0.0;
+    V[0] = q[3];
+    V[1] = odd ? q[5] : q[4];             // tube a
+    V[2] = odd ? q[4] : q[5];             // tube b
+    double rA = 0.0, rB = 0.0;
+    PairPar p;
+    double h = 0.0;
+    int left = 0;
+    bool lv3 = true;
+    uint32_t rem = pl.step;
+    for (;;) {
+        if (left == 0) {
+            if (rem == 0u) break;
+            const int k = __builtin_ctz(rem);
+            rem &= rem - 1u;
+            const SegPar sp = seg_par_at<false, false>(sy, seg_bits(sg, k));
+            p = pair_par(sp, odd);
+            h = end_lds[k * CTR_BLOCK];
+            left = n_lds[k * CTR_BLOCK];
+            lv3 = (sp.present & 4u) != 0u || sp.present == 0u;
+        }
+        if (__ballot(lv3) == 0) rk4_step_pair<2, CAREFUL>(p, h, A, B, U, V, rA, rB);
+        else rk4_step_pair<3, CAREFUL>(p, h, A, B, U, V, rA, rB);
+        st.nfev += 4;
+        st.nstep++;
+        --left;
+    }
+    // the tube-0-alone tail as segment maps (fk_lane_rk4): u = (u_x,0, 0, u_z,0), u_z,0 from the odd lane
+    const Trig tc = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    const double uzt[3] = {U[0], 0.0, 0.0};
+    uint32_t tail = pl.tail;
+    while (__ballot(tail != 0u) != 0) {
+        if (tail != 0u) {
+            const int k = __builtin_ctz(tail);
+            tail &= tail - 1u;
+            const SegPar pt = seg_par_at<false, false>(sy, seg_bits(sg, k));
+            const int n = n_lds[k * CTR_BLOCK];
+            double aq[9], am[3];
+            const int ncomp = rigid_segment_map<false>(pt, tc, uzt, end_lds[k * CTR_BLOCK], n, aq, am);
+            #pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double *X = r ? B : A;
+                double &rr = r ? rB : rA;
+                double nX[3];
+                #pragma unroll
+                for (int c = 0; c < 3; ++c) nX[c] = fma(X[2], aq[6 + c], fma(X[1], aq[3 + c], X[0] * aq[c]));
+                rr = fma(X[2], am[2], fma(X[1], am[1], fma(X[0], am[0], rr)));
+                #pragma unroll
+                for (int c = 0; c < 3; ++c) X[c] = nX[c];
+            }
+            st.nfev += 4u * (uint32_t)n;
+            st.nrej += (1u << 16) + (uint32_t)ncomp;
+        }
+    }
+    double r3[3] = {dpp_qp<DPP_FROM_EVEN>(rA), dpp_qp<DPP_FROM_EVEN>(rB), dpp_qp<DPP_FROM_ODD>(rA)};
+    if (pl.too_long) {
+        r3[0] = r3[1] = r3[2] = NAN;
+        st.status |= CTR_STATUS_TOO_LONG | CTR_STATUS_NAN;
+    }
+    tip[0] = r3[0]; tip[1] = r3[1]; tip[2] = r3[2];
     if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
 }
 

@@ -167,6 +167,20 @@ __host__ __device__ inline size_t lane_lds_bytes(const KCfg &kc)
 // The tube table episode `epoch` of env `genv` integrates with: the system row, or with domain
 // randomisation the lane's re-sampled table (epoch 0 = before the first reset: the nominal
 // table, as the reference constructor's FK, ctr_reach_env.py:65).
+// slot: this env's entry of the dynamic LDS table (the lane; both lanes of a k_step_pair env
+// share one and store the same values).
+__device__ __forceinline__ const SysK &episode_sys_at(const KCfg &kc, const SysK *s_sys, const ctr_tube_raw_t *s_raw,
+                                                      int s, uint32_t epoch, uint64_t genv, int slot)
+{
+    if (kc.c.domain_rand == 0.0 || epoch == 0) return s_sys[s];
+    SysK &me = s_lane_dyn[slot];
+    domain_system(s_sys[s], s_raw[s], kc.c.domain_rand, kc.c.seed, epoch, genv, me, nullptr);
+    #pragma unroll
+    for (int j = 0; j < 11; ++j) sysk_derive(me, j);
+    me.lut = nullptr;
+    return me;
+}
+
 __device__ __forceinline__ const SysK &episode_sys(const KCfg &kc, const SysK *s_sys, const ctr_tube_raw_t *s_raw,
                                                    int s, uint32_t epoch, uint64_t genv)
 {
@@ -715,12 +729,13 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
 // lead lane; lane 1 also holds the env's prefetched pool row (pool_prefetch<true>) and writes the
 // reset, lane 0 everything else.  Same values and the same flags as step_finish.  Every lane of
 // the wave calls it (group shuffles); ag is valid on lane 0 of the group (fk_group_rigid4).
+template <int G = SEG_GROUP>
 __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o,
                                                   int64_t e, int j, bool in, int s, const float q[6], double ag[3],
                                                   const FkStats &st, int32_t autoreset, StepFlags &fl,
                                                   const PoolPre &pp, float4 &grow)
 {
-    const int lead = (int)(threadIdx.x & 63) & ~(SEG_GROUP - 1);
+    const int lead = (int)(threadIdx.x & 63) & ~(G - 1);
     #pragma unroll
     for (int i = 0; i < 3; ++i) ag[i] = __shfl(ag[i], lead);
     if (!in || j > 1) return;
@@ -804,6 +819,42 @@ __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batc
         write_obs(o.obs, e, obs, multi, f64);
         fl.pooled = true;
         fl.pooled_r = r;
+    }
+}
+
+// The end of every step (all lanes of the wave): the auto-reset lists (miss sweep, pool refill
+// queue) and the fused push of the step's rows.
+__device__ __forceinline__ void step_epilogue(const ctr_batch_t &b, const ctr_step_out_t &o, int32_t autoreset,
+                                              const StepFlags &fl, int64_t e, bool live, const ctr_gather_push_t *gp,
+                                              bool slot_free0, float4 grow)
+{
+    if (autoreset) {
+        if (autoreset == CTR_AUTORESET_POOLED) {
+            // no miss sweep follows: zero the next step's miss counter here (this step neither
+            // reads nor appends to either counter)
+            if (blockIdx.x == 0 && threadIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;
+        } else {
+            const int32_t one[1] = {(int32_t)e};
+            wave_append(miss_counter(b), miss_items(b), b.n, fl.miss, one, 1);
+        }
+        if (b.pool_depth > 0) {
+            const int32_t two[2] = {(int32_t)e, (int32_t)(fl.pooled_r + (uint32_t)b.pool_depth)};
+            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
+        }
+    }
+    if (gp) {
+        // the fused push (every lane of the wave here): once every consumer has released the
+        // slot (normally known since the staging), each env's row into every rank's ring with
+        // system-scope stores, waited on, so the rows are performed at system scope before the
+        // wave ends and the next launch publishes the sequence words (include/ctr_reach_amd.h)
+        if (!slot_free0 && !gather_wait_slot(gp, o.gather_seq)) {
+            if ((threadIdx.x & 63) == 0) atomicOr(gp->err, CTR_GATHER_E_RELEASE_TIMEOUT);
+            gather_poison_lanes(gp, o.gather_seq);       // the overrun consumers learn it too
+        }
+        if (live) gather_store_row(gp, e, grow);
+        gather_rows_performed();
+        if (o.gather_wait_prev && blockIdx.x == 0 && threadIdx.x < 64)
+            gather_wait_prev_lane(gp, o.gather_seq - 1u);
     }
 }
 
@@ -915,48 +966,146 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
         step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, s_fin_t[threadIdx.x],
                     s_fin_ep[threadIdx.x], dg_f, grow);
     }
-    if (autoreset) {
-        if (autoreset == CTR_AUTORESET_POOLED) {
-            // no miss sweep follows: zero the next step's miss counter here (this step neither
-            // reads nor appends to either counter)
-            if (blockIdx.x == 0 && threadIdx.x == 0) b.work[(b.work_parity & 1) ^ 1] = 0;
-        } else {
-            const int32_t one[1] = {(int32_t)e};
-            wave_append(miss_counter(b), miss_items(b), b.n, fl.miss, one, 1);
-        }
-        if (b.pool_depth > 0) {
-            const int32_t two[2] = {(int32_t)e, (int32_t)(fl.pooled_r + (uint32_t)b.pool_depth)};
-            wave_append(b.refill, b.refill + 1, b.refill_cap, fl.pooled, two, 2);
-        }
+    step_epilogue(b, o, autoreset, fl, e, live, gp, slot_free0, grow);
+}
+
+// ------------------------------------------------------------------------------------------
+// BASELINE configs[4] (compliant model, fixed-step RK4, no y pre-curvature: MODE 2): one env on a
+// lane PAIR (fk_pair_rk4), 512-lane workgroups of 256 envs = 8 waves, two per SIMD (waves w and
+// w + 4 of a workgroup share a SIMD: tools/ubench/simd_map.hip).  The launch lasts as long as its
+// most loaded SIMD, so the workgroup first ranks its envs by predicted work (the RK4 steps at
+// levels 3 and 2, from the post-action extensions) and deals them so that each SIMD gets one
+// heavy and one light wave: rank chunk c (32 envs, c = 0 heaviest) goes to wave c < 4 ? c : 11 - c.
+// The result of an env does not depend on its lanes (the pair's arithmetic is self-contained).
+// ------------------------------------------------------------------------------------------
+#ifndef CTR_RK4_PAIR
+#define CTR_RK4_PAIR 1
+#endif
+template <int MODE>
+constexpr bool pair_mode() { return CTR_RK4_PAIR && MODE == 2; }
+template <int MODE>
+constexpr int step_block() { return pair_mode<MODE>() ? 2 * BLOCK : BLOCK; }
+template <int MODE>
+constexpr int step_lanes_per_env() { return pair_mode<MODE>() ? 2 : ((MODE & 6) == 6 ? SEG_GROUP : 1); }
+
+// predicted cost of an env's stepped RK4 work: level-3 steps over [0, beta_2 + L_2], level-2 steps
+// over the rest of tube 1 (relative costs 4 : 3, the steps' instruction counts); an integer key
+__device__ __forceinline__ uint32_t pair_work_key(const ctr_system_t &sy, const float q[6], double steps_per_m)
+{
+    const double e2 = fmax(0.0, (double)q[2] + sy.L[2]);
+    const double e1 = fmax(e2, (double)q[1] + sy.L[1]);
+    const double w = steps_per_m * (4.0 * e2 + 3.0 * (e1 - e2));
+    return (uint32_t)fmin(fmax(w, 0.0), 16777215.0);
+}
+
+template <bool HER>
+__device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t &b, const float *__restrict__ actions,
+                                               const ctr_step_out_t &o, int32_t autoreset, const HerK &hk)
+{
+    const ctr_her_t *her = HER ? &hk.h : nullptr;
+    constexpr int NE = BLOCK;                 // envs per 512-lane workgroup
+    __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
+    __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
+    __shared__ uint32_t s_key[NE];
+    __shared__ uint16_t s_src[NE];
+    __shared__ float s_q[6][NE];
+    __shared__ int32_t s_s[NE];
+    const int pr = (int)(threadIdx.x >> 1);
+    const int j = (int)(threadIdx.x & 1);
+    const bool odd = j != 0;
+    const int64_t base = (int64_t)blockIdx.x * NE;
+    // the natural env of this pair: its post-action joints (set_action on both lanes, the same
+    // values) and its work key
+    const int64_t en = base + pr;
+    const bool in_n = en < b.n;
+    const int64_t ec = in_n ? en : b.n - 1;
+    const int s_in = b.system[ec];
+    float q[6], a_in[6];
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * ec + i]; a_in[i] = actions[6 * ec + i]; }
+    const ctr_gather_push_t *gp = o.gather;
+    const uint32_t rel0 = gp ? gather_release_load(gp, o.gather_seq) : 0u;
+    stage_systems(kc, s_sys, s_raw);
+    const bool slot_free0 = gp ? gather_slot_free(gp, o.gather_seq, rel0) : true;
+    if (o.packed && o.packed_seq && blockIdx.x == 0 && threadIdx.x == 0)
+        *reinterpret_cast<uint4 *>(o.packed + 4 * b.n) = make_uint4(o.packed_seq, 0u, 0u, 0u);
+    if (blockIdx.x == 0) {
+        if (o.gather_prev) gather_publish_lane(o.gather_prev, o.gather_prev_seq);
+        if (gp) gather_release_lane(gp, o.gather_seq + 1u - (uint32_t)gp->depth);
     }
-    if (gp) {
-        // the fused push (every lane of the wave here): once every consumer has released the
-        // slot (normally known since the staging), each env's row into every rank's ring with
-        // system-scope stores, waited on, so the rows are performed at system scope before the
-        // wave ends and the next launch publishes the sequence words (include/ctr_reach_amd.h)
-        if (!slot_free0 && !gather_wait_slot(gp, o.gather_seq)) {
-            if ((threadIdx.x & 63) == 0) atomicOr(gp->err, CTR_GATHER_E_RELEASE_TIMEOUT);
-            gather_poison_lanes(gp, o.gather_seq);       // the overrun consumers learn it too
-        }
-        if (live) gather_store_row(gp, e, grow);
-        gather_rows_performed();
-        if (o.gather_wait_prev && blockIdx.x == 0 && threadIdx.x < 64)
-            gather_wait_prev_lane(gp, o.gather_seq - 1u);
+    const int sn = clamp_sys(s_in, kc.c.n_systems);
+    set_action_substeps(s_sys[sn], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);
+    // unique keys (work << 8 | pair), dead envs lightest
+    const uint32_t key = ((in_n ? pair_work_key(s_sys[sn], q, (double)kc.c.rk4_steps_per_m) : 0u) << 8) | (uint32_t)pr;
+    if (!odd) {
+        s_key[pr] = key;
+        #pragma unroll
+        for (int i = 0; i < 6; ++i) s_q[i][pr] = q[i];
+        s_s[pr] = sn;
     }
+    __syncthreads();
+    // rank by descending key: lane 0 of the pair counts over the first half of the keys, lane 1
+    // over the second, one DPP swap adds them
+    int cnt = 0;
+    const uint4 *k4 = reinterpret_cast<const uint4 *>(s_key) + (odd ? NE / 8 : 0);
+    #pragma unroll 8
+    for (int i = 0; i < NE / 8; ++i) {
+        const uint4 v = k4[i];
+        cnt += (v.x > key) + (v.y > key) + (v.z > key) + (v.w > key);
+    }
+    const int rank = cnt + __builtin_amdgcn_update_dpp(0, cnt, DPP_SWAP, 0xF, 0xF, false);
+    const int chunk = rank >> 5;
+    const int wave = chunk < 4 ? chunk : 11 - chunk;
+    if (!odd) s_src[wave * 32 + (rank & 31)] = (uint16_t)pr;
+    __syncthreads();
+    const int src = s_src[pr];
+    const int64_t e = base + src;
+    const bool in = e < b.n;
+    const bool live = in && !odd;
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = s_q[i][src];
+    const int s = s_s[src];
+    const int64_t ee = in ? e : b.n - 1;
+    const int32_t t_in = b.t[ee];
+    const uint32_t ep_in = b.epoch[ee];
+    StepFlags fl;
+    float4 grow = make_float4(0.f, 0.f, 0.f, 0.f);
+    PoolPre pp;
+    if (in && j == (HER ? 0 : 1)) pool_prefetch<true>(kc, b, e, autoreset, pp, t_in, ep_in);
+    const SysK &sy = in ? episode_sys_at(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e), pr) : s_sys[0];
+    const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
+    FkStats st = {0, 0, 0, 0, 0};
+    double ag[3];
+    if (fk_needs_careful_trig(qd)) fk_pair_rk4<true>(sy, qd, odd, ag, st, (double)kc.c.rk4_steps_per_m);
+    else fk_pair_rk4<false>(sy, qd, odd, ag, st, (double)kc.c.rk4_steps_per_m);
+    if constexpr (HER) {
+        if (live) {
+            double dg_in[3];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) dg_in[i] = b.desired_goal[3 * e + i];
+            step_finish(kc, b, o, e, s, q, ag, st, autoreset, fl, her, actions + 6 * e, pp, t_in, ep_in, dg_in, grow);
+        }
+    } else {
+        step_finish_group<2>(kc, b, o, e, j, in, s, q, ag, st, autoreset, fl, pp, grow);
+    }
+    step_epilogue(b, o, autoreset, fl, e, live, gp, slot_free0, grow);
 }
 
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
-                                                   ctr_step_out_t o, int32_t autoreset)
+__global__ __launch_bounds__(step_block<MODE>()) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
+                                                                ctr_step_out_t o, int32_t autoreset)
 {
-    step_body<MODE, false>(kc, b, actions, o, autoreset, HerK{});
+    if constexpr (pair_mode<MODE>()) step_body_pair<false>(kc, b, actions, o, autoreset, HerK{});
+    else step_body<MODE, false>(kc, b, actions, o, autoreset, HerK{});
 }
 
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void k_step_her(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
-                                                       ctr_step_out_t o, int32_t autoreset, HerK hk)
+__global__ __launch_bounds__(step_block<MODE>()) void k_step_her(KCfg kc, ctr_batch_t b,
+                                                                    const float *__restrict__ actions,
+                                                                    ctr_step_out_t o, int32_t autoreset, HerK hk)
 {
-    step_body<MODE, true>(kc, b, actions, o, autoreset, hk);
+    if constexpr (pair_mode<MODE>()) step_body_pair<true>(kc, b, actions, o, autoreset, hk);
+    else step_body<MODE, true>(kc, b, actions, o, autoreset, hk);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1687,14 +1836,21 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
     if (b.pool_depth > 0 && !cfg->resample_joints) return fail(CTR_EINVAL, "the reset pool needs resample_joints");
     KCfg kc = make_kcfg(cfg);
     hipStream_t s = (hipStream_t)stream;
-    const int64_t lanes = (kc.mode & 6) == 6 ? SEG_GROUP * b.n : b.n;      // k_step's lanes per env
     HerK hk = {};
     if (her) hk.h = *her;
     const int32_t her_on = her != nullptr;
-    if (her)
-        CTR_LAUNCH(k_step_her, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
-    else
-        CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+    if (kc.mode == 2 && pair_mode<2>()) {
+        // configs[4]: 256 envs per 512-lane workgroup (k_step_pair); dynamic LDS: one domain table per env
+        const dim3 g((unsigned)((b.n + BLOCK - 1) / BLOCK)), blk(step_block<2>());
+        if (her) hipLaunchKernelGGL(k_step_her<2>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
+        else hipLaunchKernelGGL(k_step<2>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+    } else {
+        const int64_t lanes = (kc.mode & 6) == 6 ? SEG_GROUP * b.n : b.n;      // k_step's lanes per env
+        if (her)
+            CTR_LAUNCH(k_step_her, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
+        else
+            CTR_LAUNCH(k_step, kc.mode, dim3(grid_for(lanes)), lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+    }
     if (int r = hip_check("ctr_step launch")) return r;
     if (autoreset == CTR_AUTORESET_SWEEP) {
         // misses are rare with a pool: a small grid sweeps the list grid-stride

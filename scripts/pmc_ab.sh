@@ -1,5 +1,5 @@
 # PMC passes of bench.py --profile-only per library variant (A/B of kernel designs).
-# usage: bash scripts/pmc_ab.sh tag lib1.so lib2.so ...   -> gpurun_out/pmcab_<tag>/<lib>/<pass>/
+# usage: [BENCH_ARGS="--config 5"] bash scripts/pmc_ab.sh tag lib1.so lib2.so ...   -> gpurun_out/pmcab_<tag>/<lib>/<pass>/
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
@@ -12,7 +12,7 @@ for v in "$@"; do
     for P in "$P1" "$P2"; do
         i=$((i+1))
         CTR_REACH_AMD_LIB=$PWD/gym-ctr-reach_amd/ctr_reach_amd/lib/$v timeout -s KILL 120 rocprofv3 --pmc $P \
-            --output-format csv -d $O/p$i -o run -- python3 bench.py --steps 10 --warmup 2 --profile-only \
+            --output-format csv -d $O/p$i -o run -- python3 bench.py --steps 10 --warmup 2 --profile-only ${BENCH_ARGS:-} \
             > $O/p$i.log 2>&1 || { echo "$v pass $i failed"; tail -5 $O/p$i.log; exit 1; }
     done
 done

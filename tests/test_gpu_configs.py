@@ -132,3 +132,32 @@ def test_bench_two_ranks_gloo_rehearsal(cuda):
     assert out["config"]["process_group"] == {"backend": "gloo", "world_size": 2}
     assert out["config"]["all_gather"]["bytes_per_env"] == 16
     assert out["config"]["steady_state"]["refills_in_window"] == 2
+
+
+@pytest.mark.parametrize("systems,rand", [([0], 0.0), ([0, 1, 2, 3], 0.0), ([0, 1, 2, 3], 0.05)])
+def test_configs4_pair_step_matches_one_lane_fk(cuda, systems, rand):
+    """configs[4]'s k_step runs each env on a lane pair (fk_pair_rk4, work-ranked inside 512-lane
+    workgroups); the FK operator (ctr_fk) runs one env per lane (fk_lane_rk4).  Same ODE and step
+    plan, the twist rounded in another order: the step's tips equal the operator's on the post-step
+    joints to rounding (<= 1e-12 m; mixed systems, domain-randomised tables, a ragged batch), and
+    the RHS counts are equal."""
+    import torch
+    from ctr_reach_amd import CtrReachVecEnv
+    n = 65536 - 77
+    env = CtrReachVecEnv(n, device=cuda, seed=4, integrator="rk4", rk4_steps_per_m=400, model="compliant",
+                         select_systems=systems, domain_rand=rand, autoreset=False)
+    env.reset()
+    rng = np.random.default_rng(8)
+    for _ in range(2):
+        env.step(torch.tensor(_acts(rng, n, env.action_space.high), device=cuda))
+    torch.cuda.synchronize()
+    tables = env.domain_parameters()["table"] if rand else None
+    tip, st = env.forward_kinematics(env.joints, None if rand else env.system, tables=tables, return_stats=True)
+    torch.cuda.synchronize()
+    assert np.abs(env.achieved_goal.cpu().numpy() - tip.cpu().numpy()).max() < 1e-12
+    env.enable_nfev()
+    env.step(torch.zeros((n, 6), device=cuda))
+    tip, st = env.forward_kinematics(env.joints, None if rand else env.system, tables=tables, return_stats=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(env.nfev.cpu().numpy(), st["nfev"].cpu().numpy())
+    assert np.abs(env.achieved_goal.cpu().numpy() - tip.cpu().numpy()).max() < 1e-12
