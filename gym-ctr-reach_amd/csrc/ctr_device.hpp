@@ -1699,13 +1699,17 @@ constexpr int DPP_FROM_ODD = 0xF5;     // quad_perm [1, 1, 3, 3]: both lanes of 
 constexpr int DPP_FROM_EVEN = 0xA0;    // quad_perm [0, 0, 2, 2]
 constexpr int DPP_SWAP = 0xB1;         // quad_perm [1, 0, 3, 2]
 
-// A segment's RHS constants in the lane's tube order (SegPar, seg_fold_inv'ed: wx = inv EI Ux).
+// A segment's RHS constants in the lane's tube order (SegPar, seg_fold_inv'ed: wx = inv EI Ux),
+// and the alpha' presence masks of slots 0, 1, 2 (stage_at): alpha' = u_z of a present tube, 0
+// otherwise.  alpha' is never formed: the masks scale the step coefficients of the alpha slots
+// instead (alpha_in = fma(u_z,in, C m, alpha), the update h/6 m), the same values for m = 1 and
+// alpha kept for m = 0, at no cost per RHS.
 struct PairPar {
     double wx0, wx1, wxa, wxb, g0, g1, ga, gb;
-    bool m0, ma, mb;        // alpha' masks (tube present) of slots 0, 1, 2
+    double ch2[3], ch[3], ch6[3];   // h/2 m, h m, h/6 m of the alpha slots (the gap's step h)
 };
 
-__device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd)
+__device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd, double h)
 {
     PairPar q;
     q.wx0 = p.wx[0];
@@ -1716,19 +1720,25 @@ __device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd)
     q.g1 = p.g[1];
     q.ga = odd ? p.g[2] : p.g[1];
     q.gb = odd ? p.g[1] : p.g[2];
-    q.m0 = (p.present & 1u) != 0u;
-    q.ma = ((p.present >> (odd ? 2 : 1)) & 1u) != 0u;
-    q.mb = ((p.present >> (odd ? 1 : 2)) & 1u) != 0u;
+    const bool m[3] = {(p.present & 1u) != 0u, ((p.present >> (odd ? 2 : 1)) & 1u) != 0u,
+                       ((p.present >> (odd ? 1 : 2)) & 1u) != 0u};
+    const double h2 = 0.5 * h, h6 = h * (1.0 / 6.0);   // rk4_step_pair's coefficients
+    #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        q.ch2[j] = m[j] ? h2 : 0.0;
+        q.ch[j] = m[j] ? h : 0.0;
+        q.ch6[j] = m[j] ? h6 : 0.0;
+    }
     return q;
 }
 
-// The pair's derivative at stage input (A, B, U, V): dA, dB (rows of R [u]x), dU (du_z), dV
-// (alpha', presence-masked u_z), in the lane's tube order; r' = (A[2], B[2]) is read by the caller.
+// The pair's derivative at stage input (A, B, U, V): dA, dB (rows of R [u]x) and dU (du_z), in the
+// lane's tube order; r' = (A[2], B[2]) and alpha' (U masked, PairPar) are the caller's.
 // Level 2 (tube 2 absent): sin/cos(alpha_1 - alpha_0) only, formed from the even lane's difference
 // (the odd lane holds tube 1 in slot 2), with the same per-lane (a, b) constants (g of tube 2 = 0).
 template <int LV, bool CAREFUL>
 __device__ __forceinline__ void rhs_pair(const PairPar &p, const double A[3], const double B[3], const double U[3],
-                                         const double V[3], double dA[3], double dB[3], double dU[3], double dV[3])
+                                         const double V[3], double dA[3], double dB[3], double dU[3])
 {
     double a, b;
     if constexpr (LV == 3) {
@@ -1777,9 +1787,6 @@ __device__ __forceinline__ void rhs_pair(const PairPar &p, const double A[3], co
         dX[1] = r2 * a - r0 * u0;
         dX[2] = r0 * b - r1 * a;
     }
-    dV[0] = p.m0 ? U[0] : 0.0;                         // stage_at (masked)
-    dV[1] = p.ma ? U[1] : 0.0;
-    dV[2] = p.mb ? U[2] : 0.0;
 }
 
 // One classical RK4 step of the pair (rk4_step's combinations; a tube's zero derivatives keep its
@@ -1788,31 +1795,34 @@ template <int LV, bool CAREFUL>
 __device__ __forceinline__ void rk4_step_pair(const PairPar &p, double h, double A[3], double B[3], double U[3],
                                               double V[3], double &rA, double &rB)
 {
-    double kA[4][3], kB[4][3], kU[4][3], kV[4][3], qA[4], qB[4];
-    double iA[3], iB[3], iU[3], iV[3];
-    rhs_pair<LV, CAREFUL>(p, A, B, U, V, kA[0], kB[0], kU[0], kV[0]);
+    // kU: the stage derivatives of u_z; uU: the stage inputs of u_z (alpha' = m u_z,in)
+    double kA[4][3], kB[4][3], kU[4][3], uU[4][3], qA[4], qB[4];
+    double iA[3], iB[3], iV[3];
+    const double h2 = 0.5 * h, h6 = h * (1.0 / 6.0);
+    const double *ch2 = p.ch2, *ch = p.ch, *ch6 = p.ch6;   // the alpha slots' coefficients, masked
+    rhs_pair<LV, CAREFUL>(p, A, B, U, V, kA[0], kB[0], kU[0]);
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) uU[0][i] = U[i];
     qA[0] = A[2];
     qB[0] = B[2];
-    const double h2 = 0.5 * h;
     #pragma unroll
     for (int st = 1; st < 4; ++st) {
         const double C = st < 3 ? h2 : h;
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            iU[i] = fma(kU[st - 1][i], C, U[i]);
-            iV[i] = fma(kV[st - 1][i], C, V[i]);
+            uU[st][i] = fma(kU[st - 1][i], C, U[i]);
+            iV[i] = fma(uU[st - 1][i], st < 3 ? ch2[i] : ch[i], V[i]);
             iA[i] = fma(kA[st - 1][i], C, A[i]);
             iB[i] = fma(kB[st - 1][i], C, B[i]);
         }
-        rhs_pair<LV, CAREFUL>(p, iA, iB, iU, iV, kA[st], kB[st], kU[st], kV[st]);
+        rhs_pair<LV, CAREFUL>(p, iA, iB, uU[st], iV, kA[st], kB[st], kU[st]);
         qA[st] = iA[2];
         qB[st] = iB[2];
     }
-    const double h6 = h * (1.0 / 6.0);
     #pragma unroll
     for (int i = 0; i < 3; ++i) {
+        V[i] = fma(ch6[i], uU[0][i] + 2.0 * (uU[1][i] + uU[2][i]) + uU[3][i], V[i]);
         U[i] = fma(h6, kU[0][i] + 2.0 * (kU[1][i] + kU[2][i]) + kU[3][i], U[i]);
-        V[i] = fma(h6, kV[0][i] + 2.0 * (kV[1][i] + kV[2][i]) + kV[3][i], V[i]);
         A[i] = fma(h6, kA[0][i] + 2.0 * (kA[1][i] + kA[2][i]) + kA[3][i], A[i]);
         B[i] = fma(h6, kB[0][i] + 2.0 * (kB[1][i] + kB[2][i]) + kB[3][i], B[i]);
     }
@@ -1855,8 +1865,8 @@ __device__ void fk_pair_rk4(const SysK &sy, const double q[6], bool odd, double 
             const int k = __builtin_ctz(rem);
             rem &= rem - 1u;
             const SegPar sp = seg_par_at<false, false>(sy, seg_bits(sg, k));
-            p = pair_par(sp, odd);
             h = end_lds[k * CTR_BLOCK];
+            p = pair_par(sp, odd, h);
             left = n_lds[k * CTR_BLOCK];
             lv3 = (sp.present & 4u) != 0u || sp.present == 0u;
         }

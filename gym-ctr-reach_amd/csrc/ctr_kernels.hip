@@ -729,11 +729,13 @@ __device__ __forceinline__ void step_finish(const KCfg &kc, const ctr_batch_t &b
 // lead lane; lane 1 also holds the env's prefetched pool row (pool_prefetch<true>) and writes the
 // reset, lane 0 everything else.  Same values and the same flags as step_finish.  Every lane of
 // the wave calls it (group shuffles); ag is valid on lane 0 of the group (fk_group_rigid4).
+// pp: lane 1's pool_prefetch of the env's next reset; a done env whose row was not prefetched
+// (pool_prefetch without ALL: only the time-limit ones) loads it here.
 template <int G = SEG_GROUP>
 __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batch_t &b, const ctr_step_out_t &o,
                                                   int64_t e, int j, bool in, int s, const float q[6], double ag[3],
                                                   const FkStats &st, int32_t autoreset, StepFlags &fl,
-                                                  const PoolPre &pp, float4 &grow)
+                                                  PoolPre &pp, float4 &grow)
 {
     const int lead = (int)(threadIdx.x & 63) & ~(G - 1);
     #pragma unroll
@@ -751,7 +753,9 @@ __device__ __forceinline__ void step_finish_group(const KCfg &kc, const ctr_batc
     const bool multi = kc.c.n_systems > 1;
     const bool f64 = kc.c.obs_f64 != 0;
     const uint32_t r = b.epoch[e] + 1;                          // reset number to take
-    // lane 1 holds the prefetched row of reset r: a pooled reset if the env is done and it is there
+    if (autoreset && done && b.pool_depth > 0 && j == 1 && !pp.loaded)
+        pool_load(b.pool + ((int64_t)(r % (uint32_t)b.pool_depth) * b.n + e), pp);
+    // lane 1 holds the row of reset r: a pooled reset if the env is done and it is there
     const bool reset = autoreset && done && b.pool_depth > 0 && j == 1 && pp.loaded && pp.pr == r;
     // lanes 0 and 1 of the group agree on the reset (shuffled while both are active)
     const bool reset_env = __shfl(reset ? 1 : 0, lead + 1) != 0;
@@ -1055,8 +1059,15 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     }
     const int rank = cnt + __builtin_amdgcn_update_dpp(0, cnt, DPP_SWAP, 0xF, 0xF, false);
     const int chunk = rank >> 5;
-    const int wave = chunk < 4 ? chunk : 11 - chunk;
-    if (!odd) s_src[wave * 32 + (rank & 31)] = (uint16_t)pr;
+#if defined(CTR_PAIR_DEAL_ADJ)          // A/B diagnostic: pair chunks onto waves 2k, 2k + 1 instead
+    const int slot = (chunk < 4 ? 2 * chunk : 2 * (7 - chunk) + 1) * 32 + (rank & 31);
+#elif defined(CTR_PAIR_NOSORT)          // A/B diagnostic: the natural env order
+    const int slot = pr;
+    (void)chunk;
+#else
+    const int slot = (chunk < 4 ? chunk : 11 - chunk) * 32 + (rank & 31);
+#endif
+    if (!odd) s_src[slot] = (uint16_t)pr;
     __syncthreads();
     const int src = s_src[pr];
     const int64_t e = base + src;
@@ -1071,7 +1082,8 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     StepFlags fl;
     float4 grow = make_float4(0.f, 0.f, 0.f, 0.f);
     PoolPre pp;
-    if (in && j == (HER ? 0 : 1)) pool_prefetch<true>(kc, b, e, autoreset, pp, t_in, ep_in);
+    // the time-limit resets' rows in flight during the FK (the others load theirs when done)
+    if (in && j == (HER ? 0 : 1)) pool_prefetch(kc, b, e, autoreset, pp, t_in, ep_in);
     const SysK &sy = in ? episode_sys_at(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e), pr) : s_sys[0];
     const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
     FkStats st = {0, 0, 0, 0, 0};
