@@ -2,8 +2,9 @@
 # Every GPU call of this repository, as phases (run through gpurun from the repo root):
 #   bash scripts/gpu.sh <phase> [<phase> ...]
 #   suite     the GPU test suite + smoke
-#   bench     headline bench x2 (+ CPU baseline once) and the two-rank gloo rehearsal on one GPU
-#             (exercises the push gather's pre-window check, calibration and post-window check)
+#   bench     headline bench x2 (+ CPU baseline once) and the two-rank gloo rehearsals on one GPU
+#             (headline and configs[4]: the push gather's pre-window check, calibration and
+#             post-window check)
 #   evidence  every bench line: headline x2, 128 steps, float64 observations, configs[1] x2,
 #             configs[4] (20 and 128 steps), mixed systems 0-3
 #   soak      reset-pool soak (tools/soak_pool.py: pooled vs synchronous resets, bit-equal)
@@ -53,6 +54,7 @@ bench)
     run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
     run bench_2 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
     TAILN=3 run bench_n2_gloo 300 env CTR_BENCH_BACKEND=gloo CTR_BENCH_SAME_DEVICE=1 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline
+    TAILN=3 run bench_c5_n2_gloo 300 env CTR_BENCH_BACKEND=gloo CTR_BENCH_SAME_DEVICE=1 python bench.py --gpus 2 --config 5 --steps 20 --warmup 5 --no-cpu-baseline
     ;;
 evidence)
     run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5

@@ -1,7 +1,8 @@
 """Captured step sequences (CtrReachVecEnv.capture_steps, one HIP graph per refill period) replay
 the same trajectory as stepping from Python: joints, goals, episode clocks, reset numbers,
 observations, rewards, done flags and the reset pool bit-exact after several replays with
-auto-resets and refills inside them (compliant scipy-RK45 and the rigid 8-lane group path)."""
+auto-resets and refills inside them (compliant scipy-RK45, the rigid 8-lane group path and
+configs[4]'s lane-pair step)."""
 import numpy as np
 import pytest
 
@@ -11,7 +12,8 @@ KEYS = ("joints", "desired_goal", "achieved_goal", "t", "epoch", "system", "obs"
         "terminal_obs", "pool_r", "pool_q0", "pool_dg")
 
 
-@pytest.mark.parametrize("n,kw", [(2048, {}), (1024, dict(integrator="rk4", rk4_steps_per_m=100, model="rigid"))])
+@pytest.mark.parametrize("n,kw", [(2048, {}), (1024, dict(integrator="rk4", rk4_steps_per_m=100, model="rigid")),
+                                  (1500, dict(integrator="rk4", rk4_steps_per_m=400, model="compliant"))])
 def test_graph_replay_matches_eager_steps(cuda, n, kw):
     import torch
     from ctr_reach_amd import CtrReachVecEnv

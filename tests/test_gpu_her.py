@@ -174,7 +174,8 @@ def test_fused_and_unfused_recording_write_identical_stores(cuda, oracle_mod):
     """The same seeds and actions through ctr_step_her (recording inside k_step) and through
     ctr_step + ctr_her_record (a second launch reading the step outputs): every store buffer is
     byte-equal, pool misses (a one-deep pool, never refilled) included."""
-    for envkw in ({}, dict(pool_depth=1, refill_interval=100000)):
+    for envkw in ({}, dict(pool_depth=1, refill_interval=100000),
+                  dict(integrator="rk4", rk4_steps_per_m=400, model="compliant")):   # the lane-pair step
         stores = []
         for fused in (True, False):
             env, her, rec = _run(cuda, n=40, steps=30, fused=fused, **envkw)

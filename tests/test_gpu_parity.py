@@ -183,15 +183,17 @@ def test_autoreset_and_terminal_obs(cuda):
     assert (np.abs(term[:, 9:12] - new[:, 9:12]).max(axis=1) > 0).mean() > 0.99
 
 
-def test_shard_invariance(cuda):
-    """Two shards with env_base offsets reproduce one big batch exactly (RNG keyed by global id)."""
+@pytest.mark.parametrize("solver", [{}, dict(integrator="rk4", rk4_steps_per_m=400, model="compliant")])
+def test_shard_invariance(cuda, solver):
+    """Two shards with env_base offsets reproduce one big batch exactly (RNG keyed by global id);
+    configs[4]'s lane-pair step too (its envs are dealt to lanes by work, per workgroup)."""
     import torch
-    n = 8192
-    full = _env(cuda, n, seed=42)
+    n = 8192 + (300 if solver else 0)
+    full = _env(cuda, n, seed=42, **solver)
     full.reset()
-    h = n // 2
-    a = _env(cuda, h, seed=42, env_base=0)
-    b = _env(cuda, h, seed=42, env_base=h)
+    h = n // 2 + (77 if solver else 0)
+    a = _env(cuda, h, seed=42, env_base=0, **solver)
+    b = _env(cuda, n - h, seed=42, env_base=h, **solver)
     a.reset(); b.reset()
     rng = np.random.default_rng(1)
     for _ in range(5):
