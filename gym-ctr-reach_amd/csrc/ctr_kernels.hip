@@ -992,14 +992,15 @@ constexpr int step_block() { return pair_mode<MODE>() ? 2 * BLOCK : BLOCK; }
 template <int MODE>
 constexpr int step_lanes_per_env() { return pair_mode<MODE>() ? 2 : ((MODE & 6) == 6 ? SEG_GROUP : 1); }
 
-// predicted cost of an env's stepped RK4 work: level-3 steps over [0, beta_2 + L_2], level-2 steps
-// over the rest of tube 1 (relative costs 4 : 3, the steps' instruction counts); an integer key
-__device__ __forceinline__ uint32_t pair_work_key(const ctr_system_t &sy, const float q[6], double steps_per_m)
+// predicted cost of an env's stepped RK4 work, relative to its bound 4 L_1: level-3 steps over
+// [0, beta_2 + L_2], level-2 steps over the rest of tube 1 (relative costs 4 : 3, the steps'
+// instruction counts), as one of 256 buckets, the heaviest first
+__device__ __forceinline__ int pair_work_bucket(const ctr_system_t &sy, const float q[6], double inv_wmax)
 {
     const double e2 = fmax(0.0, (double)q[2] + sy.L[2]);
     const double e1 = fmax(e2, (double)q[1] + sy.L[1]);
-    const double w = steps_per_m * (4.0 * e2 + 3.0 * (e1 - e2));
-    return (uint32_t)fmin(fmax(w, 0.0), 16777215.0);
+    const double w = (4.0 * e2 + 3.0 * (e1 - e2)) * inv_wmax;     // in [0, 1] for nested tubes
+    return 255 - (int)fmin(fmax(w * 255.0, 0.0), 255.0);
 }
 
 template <bool HER>
@@ -1010,7 +1011,7 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     constexpr int NE = BLOCK;                 // envs per 512-lane workgroup
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
-    __shared__ uint32_t s_key[NE];
+    __shared__ int32_t s_hist[256];         // envs per work bucket, then the buckets' first ranks
     __shared__ uint16_t s_src[NE];
     __shared__ float s_q[6][NE];
     __shared__ int32_t s_s[NE];
@@ -1029,7 +1030,8 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     for (int i = 0; i < 6; ++i) { q[i] = b.joints[6 * ec + i]; a_in[i] = actions[6 * ec + i]; }
     const ctr_gather_push_t *gp = o.gather;
     const uint32_t rel0 = gp ? gather_release_load(gp, o.gather_seq) : 0u;
-    stage_systems(kc, s_sys, s_raw);
+    if (threadIdx.x < 256) s_hist[threadIdx.x] = 0;
+    stage_systems(kc, s_sys, s_raw);         // (its barrier also orders the histogram's zeroing)
     const bool slot_free0 = gp ? gather_slot_free(gp, o.gather_seq, rel0) : true;
     if (o.packed && o.packed_seq && blockIdx.x == 0 && threadIdx.x == 0)
         *reinterpret_cast<uint4 *>(o.packed + 4 * b.n) = make_uint4(o.packed_seq, 0u, 0u, 0u);
@@ -1039,25 +1041,35 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     }
     const int sn = clamp_sys(s_in, kc.c.n_systems);
     set_action_substeps(s_sys[sn], kc.c.constrain_alpha != 0, kc.c.n_substeps, q, a_in);
-    // unique keys (work << 8 | pair), dead envs lightest
-    const uint32_t key = ((in_n ? pair_work_key(s_sys[sn], q, (double)kc.c.rk4_steps_per_m) : 0u) << 8) | (uint32_t)pr;
+    // rank by predicted work (a counting sort over 256 buckets, heaviest first, dead envs last):
+    // the bucket histogram with one LDS atomic per env -- whose return value is the env's place in
+    // its bucket (in atomic order: the deal, not any result, depends on it) -- then its prefix sums
+    double lmax = 0.0;
+    for (int k = 0; k < kc.c.n_systems; ++k) lmax = fmax(lmax, s_sys[k].L[1]);
+    const int bkt = in_n ? pair_work_bucket(s_sys[sn], q, 1.0 / (4.0 * lmax)) : 255;
+    int place = 0;
     if (!odd) {
-        s_key[pr] = key;
+        place = atomicAdd(&s_hist[bkt], 1);
         #pragma unroll
         for (int i = 0; i < 6; ++i) s_q[i][pr] = q[i];
         s_s[pr] = sn;
     }
     __syncthreads();
-    // rank by descending key: lane 0 of the pair counts over the first half of the keys, lane 1
-    // over the second, one DPP swap adds them
-    int cnt = 0;
-    const uint4 *k4 = reinterpret_cast<const uint4 *>(s_key) + (odd ? NE / 8 : 0);
-    #pragma unroll 8
-    for (int i = 0; i < NE / 8; ++i) {
-        const uint4 v = k4[i];
-        cnt += (v.x > key) + (v.y > key) + (v.z > key) + (v.w > key);
+    if (threadIdx.x < 64) {                   // wave 0: exclusive prefix sums of the 256 counts
+        const int4 c4 = reinterpret_cast<const int4 *>(s_hist)[threadIdx.x];
+        const int tot = c4.x + c4.y + c4.z + c4.w;
+        int incl = tot;
+        #pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if ((int)threadIdx.x >= off) incl += v;
+        }
+        const int ex = incl - tot;
+        reinterpret_cast<int4 *>(s_hist)[threadIdx.x] = make_int4(ex, ex + c4.x, ex + c4.x + c4.y,
+                                                                  ex + c4.x + c4.y + c4.z);
     }
-    const int rank = cnt + __builtin_amdgcn_update_dpp(0, cnt, DPP_SWAP, 0xF, 0xF, false);
+    __syncthreads();
+    const int rank = s_hist[bkt] + place;
     const int chunk = rank >> 5;
 #if defined(CTR_PAIR_DEAL_ADJ)          // A/B diagnostic: pair chunks onto waves 2k, 2k + 1 instead
     const int slot = (chunk < 4 ? 2 * chunk : 2 * (7 - chunk) + 1) * 32 + (rank & 31);
