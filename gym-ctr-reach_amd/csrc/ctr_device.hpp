@@ -1676,15 +1676,15 @@ __device__ void fk_group_rigid4(const SysK &sy, const double q[6], int j, double
 // instruction stream on different state slots:
 //   lane 0: A = R row 0, B = R row 1, rA = r_0, rB = r_1
 //   lane 1: A = R row 2,              rA = r_2                 (B, rB idle, kept at 0)
-// and each lane carries the whole twist (u_z, alpha) with tubes 1 and 2 in its own order: slot 1 is
-// tube "a" (lane 0: tube 1, lane 1: tube 2), slot 2 tube "b" (the other).  Per RHS each lane then
-// evaluates ONE table sincos, of alpha_a - alpha_0 (x = V[1] - V[0] on both lanes: no select), and
-// receives the other from its partner (one quad_perm DPP swap); the twist derivatives are written in
-// (a, b) form with per-lane constants (wx_a, wx_b, g_a, g_b), and the frame rows use the lane's own
-// u = (u_x,0, u_y,0, u_z,0).  The stage combinations and the update run on 12 slots + 2 r instead of
-// 18 values, the RHS on one sincos and two rows instead of two and three.  The two lanes' twists
-// are the reference ODE's, rounded in different orders (rounding-level apart from fk_lane_rk4's
-// one-lane arithmetic and from each other).
+// and each lane carries tube 0's twist (u_z,0, alpha_0) and that of its own tube "a" (lane 0:
+// tube 1, lane 1: tube 2; the other is tube "b").  Per RHS each lane evaluates ONE table sincos,
+// of alpha_a - alpha_0 (x = V[1] - V[0] on both lanes: no select), and receives the partner's, of
+// alpha_b - alpha_0, with one quad_perm DPP swap: so neither alpha_b nor u_z,b is needed locally.
+// The twist derivatives are written in (a, b) form with per-lane constants (wx_a, wx_b, g_a), and
+// the frame rows use the lane's own u = (u_x,0, u_y,0, u_z,0).  The stage combinations and the
+// update run on 10 slots + 2 r instead of 18 values, the RHS on one sincos and two rows instead of
+// two and three.  tube 0's twist runs on both lanes, rounded in different orders (the lanes are
+// rounding-level apart from each other and from fk_lane_rk4's one-lane arithmetic).
 // ------------------------------------------------------------------------------------------
 // quad_perm DPP on a 64-bit value: lane i of each quad reads lane P[i] (one v_mov_dpp per dword)
 template <int CTRL>
@@ -1699,14 +1699,62 @@ constexpr int DPP_FROM_ODD = 0xF5;     // quad_perm [1, 1, 3, 3]: both lanes of 
 constexpr int DPP_FROM_EVEN = 0xA0;    // quad_perm [0, 0, 2, 2]
 constexpr int DPP_SWAP = 0xB1;         // quad_perm [1, 0, 3, 2]
 
+// ctr_math::sincos_tab of one angle in two halves (the same operations, so the same bits): the
+// reduction and the table loads (pair_trig_pre), issued a stage ahead of the polynomial work that
+// consumes them (pair_trig_post), so the LDS latency of stage k + 1's table read runs under stage
+// k's RHS.  The stage-(k + 1) angle exists that early: alpha' is the masked u_z of the stage input,
+// whose value is formed before the stage's RHS.
+struct PairTrig {
+    double x, r, ts, tc;
+};
+
+__device__ __forceinline__ PairTrig pair_trig_pre(double x)
+{
+    PairTrig p;
+    p.x = x;
+    const double n = rint(x * 81.48733086305042);          // sincos_tab2_pre, angle 0
+    const int k = ((int)n) & 511;
+    p.ts = s_trig_tab[k][0];
+    p.tc = s_trig_tab[k][1];
+    p.r = fma(-n, 4.783776559169348e-19, fma(-n, 0.01227184630308513, x));
+    return p;
+}
+
+template <bool CAREFUL>
+__device__ __forceinline__ void pair_trig_post(const PairTrig &p, double &s, double &c)
+{
+    const double r = p.r, z = r * r;                        // sincos_tab2_post, angle 0
+    const double sp = fma(z, 8.3333333333333332e-03, -1.6666666666666666e-01);
+    const double cp = fma(z, 4.1666666666666664e-02, -0.5);
+    const double sr = fma(r * z, sp, r), cr = fma(z, cp, 1.0);
+    s = fma(p.ts, cr, p.tc * sr);
+    c = fma(p.tc, cr, -(p.ts * sr));
+    if (CAREFUL && __builtin_expect(__ballot(ctr_math::sincos_needs_slow(p.x)) != 0, 0) &&
+        ctr_math::sincos_needs_slow(p.x)) {
+        const ctr_math::SinCos q = ctr_math::sincos_slow(p.x);
+        s = q.s;
+        c = q.c;
+    }
+}
+
+// The angle each lane evaluates at level LV from the stage input's alpha slots: alpha_a - alpha_0
+// (level 3), or the even lane's alpha_1 - alpha_0 (level 2: the odd lane's tube a is tube 2)
+template <int LV>
+__device__ __forceinline__ double pair_angle(const double V[2])
+{
+    if constexpr (LV == 3) return V[1] - V[0];
+    else return dpp_qp<DPP_FROM_EVEN>(V[1] - V[0]);
+}
+
 // A segment's RHS constants in the lane's tube order (SegPar, seg_fold_inv'ed: wx = inv EI Ux),
-// and the alpha' presence masks of slots 0, 1, 2 (stage_at): alpha' = u_z of a present tube, 0
-// otherwise.  alpha' is never formed: the masks scale the step coefficients of the alpha slots
-// instead (alpha_in = fma(u_z,in, C m, alpha), the update h/6 m), the same values for m = 1 and
-// alpha kept for m = 0, at no cost per RHS.
+// and the alpha' presence masks of the twist slots 0 (tube 0) and 1 (tube a) (stage_at): alpha' =
+// u_z of a present tube, 0 otherwise.  alpha' is never formed: the masks scale the step
+// coefficients of the alpha slots instead (alpha_in = fma(u_z,in, C m, alpha), the update h/6 m),
+// the same values for m = 1 and alpha kept for m = 0, at no cost per RHS.
+constexpr int PAIR_NT = 2;          // twist slots per lane: tube 0, tube a
 struct PairPar {
-    double wx0, wx1, wxa, wxb, g0, g1, ga, gb;
-    double ch2[3], ch[3], ch6[3];   // h/2 m, h m, h/6 m of the alpha slots (the gap's step h)
+    double wx0, wx1, wxa, wxb, g0, ga;
+    double ch2[PAIR_NT], ch[PAIR_NT], ch6[PAIR_NT];   // h/2 m, h m, h/6 m of the alpha slots (the gap's h)
 };
 
 __device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd, double h)
@@ -1717,14 +1765,11 @@ __device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd, double h)
     q.wxa = odd ? p.wx[2] : p.wx[1];
     q.wxb = odd ? p.wx[1] : p.wx[2];
     q.g0 = p.g[0];
-    q.g1 = p.g[1];
     q.ga = odd ? p.g[2] : p.g[1];
-    q.gb = odd ? p.g[1] : p.g[2];
-    const bool m[3] = {(p.present & 1u) != 0u, ((p.present >> (odd ? 2 : 1)) & 1u) != 0u,
-                       ((p.present >> (odd ? 1 : 2)) & 1u) != 0u};
+    const bool m[PAIR_NT] = {(p.present & 1u) != 0u, ((p.present >> (odd ? 2 : 1)) & 1u) != 0u};
     const double h2 = 0.5 * h, h6 = h * (1.0 / 6.0);   // rk4_step_pair's coefficients
     #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < PAIR_NT; ++j) {
         q.ch2[j] = m[j] ? h2 : 0.0;
         q.ch[j] = m[j] ? h : 0.0;
         q.ch6[j] = m[j] ? h6 : 0.0;
@@ -1732,48 +1777,32 @@ __device__ __forceinline__ PairPar pair_par(const SegPar &p, bool odd, double h)
     return q;
 }
 
-// The pair's derivative at stage input (A, B, U, V): dA, dB (rows of R [u]x) and dU (du_z), in the
-// lane's tube order; r' = (A[2], B[2]) and alpha' (U masked, PairPar) are the caller's.
+// The pair's derivative at stage input (A, B, U, V): dA, dB (rows of R [u]x) and dU (du_z of tube 0
+// and tube a); r' = (A[2], B[2]) and alpha' (U masked, PairPar) are the caller's.
 // Level 2 (tube 2 absent): sin/cos(alpha_1 - alpha_0) only, formed from the even lane's difference
-// (the odd lane holds tube 1 in slot 2), with the same per-lane (a, b) constants (g of tube 2 = 0).
+// (the odd lane's tube a is tube 2, constant at this level: g_a = 0).
 template <int LV, bool CAREFUL>
-__device__ __forceinline__ void rhs_pair(const PairPar &p, const double A[3], const double B[3], const double U[3],
-                                         const double V[3], double dA[3], double dB[3], double dU[3])
+__device__ __forceinline__ void rhs_pair(const PairPar &p, const PairTrig &tg, const double A[3], const double B[3],
+                                         const double U[PAIR_NT], double dA[3], double dB[3], double dU[PAIR_NT])
 {
     double a, b;
     if constexpr (LV == 3) {
-        const double x = V[1] - V[0];                  // alpha_a - alpha_0
-        double sa, ca;
-        ctr_math::sincos_tab(x, s_trig_tab, sa, ca);
-        if (CAREFUL && __builtin_expect(__ballot(ctr_math::sincos_needs_slow(x)) != 0, 0) &&
-            ctr_math::sincos_needs_slow(x)) {
-            const ctr_math::SinCos r = ctr_math::sincos_slow(x);
-            sa = r.s;
-            ca = r.c;
-        }
+        double sa, ca;                                 // alpha_a - alpha_0
+        pair_trig_post<CAREFUL>(tg, sa, ca);
         const double sb = dpp_qp<DPP_SWAP>(sa), cb = dpp_qp<DPP_SWAP>(ca);   // alpha_b - alpha_0
         const double sab = sa * cb - ca * sb;          // sin(alpha_a - alpha_b)
         const double sy1 = fma(p.wxb, sb, p.wxa * sa); // u_y,0 (wx_1 s10 + wx_2 s20)
         dU[0] = -(p.g0 * sy1);
         dU[1] = p.ga * fma(p.wxb, sab, p.wx0 * sa);
-        dU[2] = p.gb * fma(-p.wxa, sab, p.wx0 * sb);
         a = fma(p.wxb, cb, fma(p.wxa, ca, p.wx0));
         b = sy1;
     } else {
-        const double x = dpp_qp<DPP_FROM_EVEN>(V[1] - V[0]);   // alpha_1 - alpha_0 (the even lane's)
-        double s1, c1;
-        ctr_math::sincos_tab(x, s_trig_tab, s1, c1);
-        if (CAREFUL && __builtin_expect(__ballot(ctr_math::sincos_needs_slow(x)) != 0, 0) &&
-            ctr_math::sincos_needs_slow(x)) {
-            const ctr_math::SinCos r = ctr_math::sincos_slow(x);
-            s1 = r.s;
-            c1 = r.c;
-        }
+        double s1, c1;                                 // alpha_1 - alpha_0 (the even lane's)
+        pair_trig_post<CAREFUL>(tg, s1, c1);
         const double sy1 = p.wx1 * s1;                 // rhs_core_lv<2>
         const double sy2 = -(p.wx0 * s1);
         dU[0] = -(p.g0 * sy1);
         dU[1] = -(p.ga * sy2);                          // tube 1 on the even lane, tube 2 (g = 0) on the odd
-        dU[2] = -(p.gb * sy2);
         a = fma(p.wx1, c1, p.wx0);
         b = sy1;
     }
@@ -1792,37 +1821,51 @@ __device__ __forceinline__ void rhs_pair(const PairPar &p, const double A[3], co
 // One classical RK4 step of the pair (rk4_step's combinations; a tube's zero derivatives keep its
 // slots exactly, so level 2 runs every slot).
 template <int LV, bool CAREFUL>
-__device__ __forceinline__ void rk4_step_pair(const PairPar &p, double h, double A[3], double B[3], double U[3],
-                                              double V[3], double &rA, double &rB)
+__device__ __forceinline__ void rk4_step_pair(const PairPar &p, double h, double A[3], double B[3], double U[PAIR_NT],
+                                              double V[PAIR_NT], double &rA, double &rB)
 {
     // kU: the stage derivatives of u_z; uU: the stage inputs of u_z (alpha' = m u_z,in)
-    double kA[4][3], kB[4][3], kU[4][3], uU[4][3], qA[4], qB[4];
-    double iA[3], iB[3], iV[3];
+    double kA[4][3], kB[4][3], kU[4][PAIR_NT], uU[4][PAIR_NT], qA[4], qB[4];
+    double iA[3], iB[3], iV[PAIR_NT];
     const double h2 = 0.5 * h, h6 = h * (1.0 / 6.0);
     const double *ch2 = p.ch2, *ch = p.ch, *ch6 = p.ch6;   // the alpha slots' coefficients, masked
-    rhs_pair<LV, CAREFUL>(p, A, B, U, V, kA[0], kB[0], kU[0]);
+    // stage 0's table read, and stage 1's (its alpha input is fma(u_z, h/2 m, alpha)) behind it
     #pragma unroll
-    for (int i = 0; i < 3; ++i) uU[0][i] = U[i];
+    for (int i = 0; i < PAIR_NT; ++i) uU[0][i] = U[i];
+    PairTrig tg = pair_trig_pre(pair_angle<LV>(V));
+    #pragma unroll
+    for (int i = 0; i < PAIR_NT; ++i) iV[i] = fma(uU[0][i], ch2[i], V[i]);
+    PairTrig tn = pair_trig_pre(pair_angle<LV>(iV));
+    rhs_pair<LV, CAREFUL>(p, tg, A, B, U, kA[0], kB[0], kU[0]);
     qA[0] = A[2];
     qB[0] = B[2];
     #pragma unroll
     for (int st = 1; st < 4; ++st) {
         const double C = st < 3 ? h2 : h;
+        tg = tn;
+        #pragma unroll
+        for (int i = 0; i < PAIR_NT; ++i) uU[st][i] = fma(kU[st - 1][i], C, U[i]);
+        if (st < 3) {                                  // the next stage's angle and table read
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) iV[i] = fma(uU[st][i], st < 2 ? ch2[i] : ch[i], V[i]);
+            tn = pair_trig_pre(pair_angle<LV>(iV));
+        }
         #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            uU[st][i] = fma(kU[st - 1][i], C, U[i]);
-            iV[i] = fma(uU[st - 1][i], st < 3 ? ch2[i] : ch[i], V[i]);
             iA[i] = fma(kA[st - 1][i], C, A[i]);
             iB[i] = fma(kB[st - 1][i], C, B[i]);
         }
-        rhs_pair<LV, CAREFUL>(p, iA, iB, uU[st], iV, kA[st], kB[st], kU[st]);
+        rhs_pair<LV, CAREFUL>(p, tg, iA, iB, uU[st], kA[st], kB[st], kU[st]);
         qA[st] = iA[2];
         qB[st] = iB[2];
     }
     #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < PAIR_NT; ++i) {
         V[i] = fma(ch6[i], uU[0][i] + 2.0 * (uU[1][i] + uU[2][i]) + uU[3][i], V[i]);
         U[i] = fma(h6, kU[0][i] + 2.0 * (kU[1][i] + kU[2][i]) + kU[3][i], U[i]);
+    }
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
         A[i] = fma(h6, kA[0][i] + 2.0 * (kA[1][i] + kA[2][i]) + kA[3][i], A[i]);
         B[i] = fma(h6, kB[0][i] + 2.0 * (kB[1][i] + kB[2][i]) + kB[3][i], B[i]);
     }
@@ -1846,13 +1889,12 @@ __device__ void fk_pair_rk4(const SysK &sy, const double q[6], bool odd, double 
     double s0, c0;
     sincos_lds(q[3], s0, c0);
     // R0 = Rz(alpha_0): rows (c0, -s0, 0), (s0, c0, 0), (0, 0, 1)
-    double A[3], B[3], U[3], V[3];
+    double A[3], B[3], U[PAIR_NT], V[PAIR_NT];
     A[0] = odd ? 0.0 : c0;  A[1] = odd ? 0.0 : -s0;  A[2] = odd ? 1.0 : 0.0;
     B[0] = odd ? 0.0 : s0;  B[1] = odd ? 0.0 : c0;   B[2] = 0.0;
-    U[0] = U[1] = U[2] = 0.0;
+    U[0] = U[1] = 0.0;
     V[0] = q[3];
     V[1] = odd ? q[5] : q[4];             // tube a
-    V[2] = odd ? q[4] : q[5];             // tube b
     double rA = 0.0, rB = 0.0;
     PairPar p;
     double h = 0.0;
