@@ -61,9 +61,13 @@ PEAK_HBM = 8000.0       # GB/s (spec)
 # algorithmic bytes per env-step of this layout: reads system 4, joints 24, actions 24, epoch 4,
 # t 4, desired goal 24 (f64) = 84; writes joints 24, achieved goal 24 (f64), t 4, obs 52, reward 4,
 # done 1, success 1, error 4, status 4 = 118.  SURVEY.md 8(d)'s 170 B assumed float32 goals and
-# no system / epoch / status words.  Auto-resets add a pooled reset row (108 B) per reset.
+# no system / epoch / status words.  An auto-reset adds its pooled reset (the 108 B of fields of a
+# ctr_pool_slot_t) read, and written: the terminal observation (13 x 4 B, or x 8 with float64
+# observations), the terminal achieved goal 24, the new desired goal 24, system 4, epoch 4 (the
+# bench env records no info buffers).
 BYTES_STEP = 84 + 118
 BYTES_RESET = 108
+BYTES_RESET_WRITE_FIXED = 24 + 24 + 4 + 4
 
 
 def parse():
@@ -725,6 +729,14 @@ def main():
             out["roofline"]["traffic"] = t.get("bytes_per_launch")
             out["roofline"]["traffic_source"] = "profiles/%s: %s" % (os.path.basename(tr), t.get("note", ""))
             out["roofline"]["traffic_over_algorithmic"] = t.get("bytes_per_launch") / (BYTES_STEP * n)
+            # the PMC passes run the window's pooled steps, so their bytes include the auto-resets at
+            # the window's rate: the algorithmic bytes of those resets beside them
+            if resets:
+                per_reset = BYTES_RESET + BYTES_RESET_WRITE_FIXED + 13 * (8 if args.obs_dtype == "float64" else 4)
+                alg_r = BYTES_STEP * n + per_reset * resets / args.steps
+                out["roofline"]["bytes_per_launch_algorithmic_with_resets"] = alg_r
+                out["roofline"]["bytes_per_reset_algorithmic"] = per_reset
+                out["roofline"]["traffic_over_algorithmic_with_resets"] = t.get("bytes_per_launch") / alg_r
     if not args.no_cpu_baseline and ws == 1:
         out["parity"] = parity_probe(env, cfgd)
         out["cpu_baseline"] = cpu_baseline(args, cfgd)
