@@ -1011,7 +1011,8 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     constexpr int NE = BLOCK;                 // envs per 512-lane workgroup
     __shared__ SysK s_sys[CTR_MAX_SYSTEMS];
     __shared__ ctr_tube_raw_t s_raw[CTR_MAX_SYSTEMS];
-    __shared__ int32_t s_hist[256];         // envs per work bucket, then the buckets' first ranks
+    __shared__ __attribute__((aligned(16))) int32_t s_hist[256];   // envs per work bucket, then the
+                                                                    // buckets' first ranks (read as int4)
     __shared__ uint16_t s_src[NE];
     __shared__ float s_q[6][NE];
     __shared__ int32_t s_s[NE];
