@@ -1955,6 +1955,340 @@ __device__ void fk_pair_rk4(const SysK &sy, const double q[6], bool odd, double 
 }
 
 // ------------------------------------------------------------------------------------------
+// scipy RK45 of the compliant model (no y pre-curvature) on a lane PAIR: fk_lane<false, false,
+// false, CAREFUL> in fk_pair_rk4's slots (A, B, U, V, rA, rB).  The controller (t, h, accept /
+// reject, the segment cursor) runs on both lanes with the same values: every norm is the sum of
+// the two lanes' partial sums, exchanged with one DPP swap (a + b == b + a exactly), so the pair
+// takes every branch together.  As in fk_lane, u_z of an absent tube a is parked (uzf) and tube
+// 0's alpha' is masked by its presence m0.  The FSAL derivative f is (fA, fB, fU); its alpha' and
+// r' are implied by y.  Each stage's table read is issued a stage early (rk4_step_pair).
+// An A/B experiment (CTR_RK45_PAIR, off in the product build): the step-path parity tests pass on
+// it, but k_step takes 92.5-95.5 us against 72.3 us one env per lane -- 1.41x the VALU
+// instructions at a 7 % better issue rate ("RK45 on lane pairs").
+// ------------------------------------------------------------------------------------------
+namespace rk {
+constexpr double RKA[6][5] = {{0, 0, 0, 0, 0},
+                              {A10, 0, 0, 0, 0},
+                              {A20, A21, 0, 0, 0},
+                              {A30, A31, A32, 0, 0},
+                              {A40, A41, A42, A43, 0},
+                              {A50, A51, A52, A53, A54}};
+constexpr double RKB[6] = {B0, 0.0, B2, B3, B4, B5};
+constexpr double RKE[6] = {E0, 0.0, E2, E3, E4, E5};
+}  // namespace rk
+
+// One attempt of RungeKutta._step_impl (rk.py:111-175) on the pair at tube level LV (3, or 2:
+// no lane of the wave has tube 2); fk_lane's attempt in the pair's slots.
+template <int LV, bool CAREFUL>
+__device__ __forceinline__ void rk45_attempt_pair(const PairPar &p, bool m0, bool odd, double A[3], double B[3],
+                                                  double U[PAIR_NT], double V[PAIR_NT], double &rA, double &rB,
+                                                  double fA[3], double fB[3], double fU[PAIR_NT], double &t, double tb,
+                                                  double &ha, double h, double tnew, bool &rejected, bool &new_step,
+                                                  bool &need_init, FkStats &st)
+{
+    using namespace rk;
+    // The stages are h-scaled (K_j = h f_j): rhs_pair at wx h and u_z,0 h gives h dA, h dB, h dU
+    // directly, so every combination's coefficient is a tableau constant (no per-lane a_sj h).
+    // Each K_j enters y_new (5th order) and the error sum as soon as it exists (fma chains from
+    // stage 0 up, fk_lane's order), so a stage is dead after its last stage input.
+    PairPar ph = p;
+    ph.wx0 = p.wx0 * h; ph.wx1 = p.wx1 * h; ph.wxa = p.wxa * h; ph.wxb = p.wxb * h;
+    double kA[3][5], kB[3][5], kU[PAIR_NT][5], al[PAIR_NT][5];   // al: h alpha' = h (masked u_z of the stage input)
+    double nA[3], nB[3], nU[PAIR_NT], nV[PAIR_NT];
+    double eA[3], eB[3], eU[PAIR_NT], eV[PAIR_NT];
+    al[0][0] = m0 ? U[0] * h : 0.0;
+    al[1][0] = U[1] * h;
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        kA[i][0] = fA[i] * h; kB[i][0] = fB[i] * h;
+        nA[i] = fma(kA[i][0], B0, A[i]); nB[i] = fma(kB[i][0], B0, B[i]);
+        eA[i] = kA[i][0] * E0; eB[i] = kB[i][0] * E0;
+    }
+    #pragma unroll
+    for (int i = 0; i < PAIR_NT; ++i) {
+        kU[i][0] = fU[i] * h;
+        nU[i] = fma(kU[i][0], B0, U[i]); eU[i] = kU[i][0] * E0;
+        nV[i] = fma(al[i][0], B0, V[i]); eV[i] = al[i][0] * E0;
+    }
+    double br[2] = {A[2] * B0, B[2] * B0}, er[2] = {A[2] * E0, B[2] * E0};
+    double iA[3], iB[3], iU[PAIR_NT], iV[PAIR_NT];
+    #pragma unroll
+    for (int i = 0; i < PAIR_NT; ++i) iV[i] = fma(al[i][0], A10, V[i]);
+    PairTrig tg = pair_trig_pre(pair_angle<LV>(iV)), tn;
+    #pragma unroll
+    for (int s = 1; s < 6; ++s) {
+        // stage s input: u_z first (alpha'_s), then the next angle's table read, then the rows
+        #pragma unroll
+        for (int i = 0; i < PAIR_NT; ++i) {
+            double u = U[i];
+            #pragma unroll
+            for (int j = 0; j < s; ++j) u = fma(kU[i][j], RKA[s][j], u);
+            iU[i] = u;
+        }
+        const double u0h = iU[0] * h;
+        const double als[PAIR_NT] = {m0 ? u0h : 0.0, iU[1] * h};
+        if (s < 5) {
+            al[0][s] = als[0];
+            al[1][s] = als[1];
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) {
+                double v = V[i];
+                #pragma unroll
+                for (int j = 0; j <= s; ++j) v = fma(al[i][j], RKA[s + 1][j], v);
+                iV[i] = v;
+            }
+            tn = pair_trig_pre(pair_angle<LV>(iV));
+        }
+        if (s > 1) {
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) { nV[i] = fma(als[i], RKB[s], nV[i]); eV[i] = fma(als[i], RKE[s], eV[i]); }
+        }
+        if (s == 5) tn = pair_trig_pre(pair_angle<LV>(nV));
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double a = A[i], b = B[i];
+            #pragma unroll
+            for (int j = 0; j < s; ++j) { a = fma(kA[i][j], RKA[s][j], a); b = fma(kB[i][j], RKA[s][j], b); }
+            iA[i] = a;
+            iB[i] = b;
+        }
+        double dA[3], dB[3], dU[PAIR_NT];
+        const double uh[PAIR_NT] = {u0h, 0.0};
+        rhs_pair<LV, CAREFUL>(ph, tg, iA, iB, uh, dA, dB, dU);
+        if (s < 5) {
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) { kA[i][s] = dA[i]; kB[i][s] = dB[i]; }
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) kU[i][s] = dU[i];
+        }
+        if (s > 1) {
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                nA[i] = fma(dA[i], RKB[s], nA[i]); nB[i] = fma(dB[i], RKB[s], nB[i]);
+                eA[i] = fma(dA[i], RKE[s], eA[i]); eB[i] = fma(dB[i], RKE[s], eB[i]);
+            }
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) { nU[i] = fma(dU[i], RKB[s], nU[i]); eU[i] = fma(dU[i], RKE[s], eU[i]); }
+            br[0] += iA[2] * RKB[s]; br[1] += iB[2] * RKB[s];
+            er[0] += iA[2] * RKE[s]; er[1] += iB[2] * RKE[s];
+        }
+        tg = tn;
+    }
+    double nr[2];
+    nr[0] = rA + h * br[0];
+    nr[1] = rB + h * br[1];
+    double k6A[3], k6B[3], k6U[PAIR_NT];       // f at y_new (unscaled: the next attempt's f)
+    rhs_pair<LV, CAREFUL>(p, tg, nA, nB, nU, k6A, k6B, k6U);
+    st.nfev += 6;
+    // error norm: this lane's slots (tube 0's twist counted on the even lane only), then the pair's sum
+    const double e6h = E6 * h;
+    auto term = [&](double k6, double e, double y, double yn) {
+        const double x = fma(k6, e6h, e) * ctr_math::rcp_est(fma(ctr_math::absmax(y, yn), RTOL, ATOL));
+        return x * x;
+    };
+    double acc[3] = {0.0, 0.0, 0.0};
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        acc[0] += term(k6A[i], eA[i], A[i], nA[i]);
+        acc[1] += term(k6B[i], eB[i], B[i], nB[i]);
+    }
+    acc[2] += term(nA[2], er[0] * h, rA, nr[0]);
+    acc[2] += term(nB[2], er[1] * h, rB, nr[1]);
+    {
+        const double tu0 = term(k6U[0], eU[0], U[0], nU[0]);
+        const double tv0 = term(m0 ? nU[0] : 0.0, eV[0], V[0], nV[0]);
+        acc[0] += odd ? 0.0 : tu0;
+        acc[1] += odd ? 0.0 : tv0;
+        acc[2] += term(k6U[1], eU[1], U[1], nU[1]);
+        acc[2] += term(nU[1], eV[1], V[1], nV[1]);
+    }
+    const double own = (acc[0] + acc[1]) + acc[2];
+    const double en2 = own + dpp_qp<DPP_SWAP>(own);   // = 18 error_norm^2
+    const double en2n = en2 * (1.0 / 18);
+    const double fpow = 0.9 * ctr_math::inv_root10(en2n);
+    const bool ok = en2n < 1.0;
+    double factor = (en2n == 0.0) ? 10.0 : fmin(10.0, fpow);
+    if (rejected) factor = fmin(1.0, factor);
+    ha *= ok ? factor : fmax(0.2, fpow);
+    if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+        #pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            nA[i] = ok ? nA[i] : A[i];
+            nB[i] = ok ? nB[i] : B[i];
+            k6A[i] = ok ? k6A[i] : fA[i];
+            k6B[i] = ok ? k6B[i] : fB[i];
+        }
+        #pragma unroll
+        for (int i = 0; i < PAIR_NT; ++i) {
+            nU[i] = ok ? nU[i] : U[i];
+            nV[i] = ok ? nV[i] : V[i];
+            k6U[i] = ok ? k6U[i] : fU[i];
+        }
+        nr[0] = ok ? nr[0] : rA;
+        nr[1] = ok ? nr[1] : rB;
+        tnew = ok ? tnew : t;
+    }
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) { A[i] = nA[i]; B[i] = nB[i]; fA[i] = k6A[i]; fB[i] = k6B[i]; }
+    #pragma unroll
+    for (int i = 0; i < PAIR_NT; ++i) { U[i] = nU[i]; V[i] = nV[i]; fU[i] = k6U[i]; }
+    rA = nr[0];
+    rB = nr[1];
+    t = tnew;
+    st.nstep += ok ? 1u : 0u;
+    st.nrej += ok ? 0u : 1u;
+    new_step = ok;
+    rejected = ok ? rejected : true;
+    if (ok && t - tb >= 0.0) need_init = true;
+}
+
+// fk_lane<false, false, false, CAREFUL> on a lane pair (see above).  Both lanes of every pair of
+// the wave call it; the tip and the counters are returned on both lanes.
+template <bool CAREFUL>
+__device__ void fk_pair_rk45(const SysK &sy, const double q[6], bool odd, double tip[3], FkStats &st)
+{
+    using namespace rk;
+    const double beta[3] = {q[0], q[1], q[2]};
+    const int col = (int)(threadIdx.x >> 1);
+    double *end_lds = &s_seg_end[0][col];
+    const Seg sg = seg_build<CTR_BLOCK, 1>(sy, beta, end_lds);
+    double A[3], B[3], U[PAIR_NT], V[PAIR_NT];
+    {
+        double s0, c0;
+        ctr_math::sincos_cw(q[3], &s0, &c0);                  // R0 = Rz(alpha_0), as fk_lane
+        A[0] = odd ? 0.0 : c0;  A[1] = odd ? 0.0 : -s0;  A[2] = odd ? 1.0 : 0.0;
+        B[0] = odd ? 0.0 : s0;  B[1] = odd ? 0.0 : c0;   B[2] = 0.0;
+    }
+    U[0] = U[1] = 0.0;
+    V[0] = q[3];
+    V[1] = odd ? q[5] : q[4];             // tube a
+    double rA = 0.0, rB = 0.0, uzf = 0.0;
+    double fA[3], fB[3], fU[PAIR_NT];
+    PairPar p;
+    bool m0 = true, lv3 = true;
+    double t = 0.0, tb = 0.0, ha = 0.0, min_step = 0.0, prev_end = 0.0;
+    uint32_t remaining = sg.kept;
+    bool need_init = true, new_step = true, rejected = false;
+    for (;;) {
+        if (need_init) {
+            if (remaining == 0u) break;
+            const int k = __builtin_ctz(remaining);
+            remaining &= remaining - 1u;
+            const SegPar sp = seg_par_at<false, false>(sy, seg_bits(sg, k));
+            p = pair_par(sp, odd, 0.0);
+            m0 = (sp.present & 1u) != 0u;
+            const bool ma = ((sp.present >> (odd ? 2 : 1)) & 1u) != 0u;
+            uzf = (!ma && U[1] != 0.0) ? U[1] : uzf;
+            U[1] = ma ? U[1] : 0.0;
+            lv3 = (sp.present & 4u) != 0u;
+            const double endk = end_lds[k * CTR_BLOCK];
+            const double a = prev_end, b = endk - 1e-6;          // model.py:141 linspace endpoints
+            const double t0 = fmin(a, b);
+            tb = fmax(a, b);
+            prev_end = endk;
+            // f = fun(t0, y0) (the level-3 form: the same values at every level)
+            rhs_pair<3, CAREFUL>(p, pair_trig_pre(pair_angle<3>(V)), A, B, U, fA, fB, fU);
+            st.nfev++;
+            st.nseg++;
+            const double interval = tb - t0;
+            if (interval == 0.0) continue;
+            if (sp.present == 0u) {                              // a gap with no tube (fk_lane)
+                rA = rB = NAN;
+                st.status |= CTR_STATUS_NAN;
+                break;
+            }
+            // select_initial_step (common.py:68-140) on the pair's slots
+            const double fV[PAIR_NT] = {m0 ? U[0] : 0.0, U[1]};
+            const double yur1 = ma ? U[1] : uzf;                 // the reference's u_z of tube a
+            double iscA[3], iscB[3], iscU[PAIR_NT], iscV[PAIR_NT], iscr[2];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                iscA[i] = ctr_math::rcp_est(ATOL + fabs(A[i]) * RTOL);
+                iscB[i] = ctr_math::rcp_est(ATOL + fabs(B[i]) * RTOL);
+            }
+            iscU[0] = ctr_math::rcp_est(ATOL + fabs(U[0]) * RTOL);
+            iscU[1] = ctr_math::rcp_est(ATOL + fabs(yur1) * RTOL);
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) iscV[i] = ctr_math::rcp_est(ATOL + fabs(V[i]) * RTOL);
+            iscr[0] = ctr_math::rcp_est(ATOL + fabs(rA) * RTOL);
+            iscr[1] = ctr_math::rcp_est(ATOL + fabs(rB) * RTOL);
+            auto sq = [](double x) { return x * x; };
+            double s0 = 0.0, s1 = 0.0;
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                s0 += sq(A[i] * iscA[i]) + sq(B[i] * iscB[i]);
+                s1 += sq(fA[i] * iscA[i]) + sq(fB[i] * iscB[i]);
+            }
+            s0 += sq(rA * iscr[0]) + sq(rB * iscr[1]) + sq(yur1 * iscU[1]) + sq(V[1] * iscV[1]);
+            s1 += sq(A[2] * iscr[0]) + sq(B[2] * iscr[1]) + sq(fU[1] * iscU[1]) + sq(fV[1] * iscV[1]);
+            s0 += odd ? 0.0 : sq(U[0] * iscU[0]) + sq(V[0] * iscV[0]);
+            s1 += odd ? 0.0 : sq(fU[0] * iscU[0]) + sq(fV[0] * iscV[0]);
+            s0 += dpp_qp<DPP_SWAP>(s0);
+            s1 += dpp_qp<DPP_SWAP>(s1);
+            const double d0sq = s0 * (1.0 / 18), d1sq = s1 * (1.0 / 18);
+            const double h0n = 0.01 * ctr_math::sqrt_rsq(s0 * ctr_math::rcp1(s1));
+            double h0 = (d0sq < 1e-10 || d1sq < 1e-10) ? 1e-6 : h0n;
+            h0 = fmin(h0, interval);
+            double A1[3], B1[3], U1[PAIR_NT], V1[PAIR_NT];
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) { A1[i] = A[i] + h0 * fA[i]; B1[i] = B[i] + h0 * fB[i]; }
+            #pragma unroll
+            for (int i = 0; i < PAIR_NT; ++i) { U1[i] = U[i] + h0 * fU[i]; V1[i] = V[i] + h0 * fV[i]; }
+            double gA[3], gB[3], gU[PAIR_NT];
+            rhs_pair<3, CAREFUL>(p, pair_trig_pre(pair_angle<3>(V1)), A1, B1, U1, gA, gB, gU);
+            st.nfev++;
+            const double gV[PAIR_NT] = {m0 ? U1[0] : 0.0, U1[1]};
+            double s2 = 0.0;
+            #pragma unroll
+            for (int i = 0; i < 3; ++i) s2 += sq((gA[i] - fA[i]) * iscA[i]) + sq((gB[i] - fB[i]) * iscB[i]);
+            s2 += sq((A1[2] - A[2]) * iscr[0]) + sq((B1[2] - B[2]) * iscr[1]) + sq((gU[1] - fU[1]) * iscU[1]) +
+                  sq((gV[1] - fV[1]) * iscV[1]);
+            s2 += odd ? 0.0 : sq((gU[0] - fU[0]) * iscU[0]) + sq((gV[0] - fV[0]) * iscV[0]);
+            s2 += dpp_qp<DPP_SWAP>(s2);
+            const double ih0 = ctr_math::rcp1(h0);
+            const double d2sq = s2 * (1.0 / 18) * ih0 * ih0;
+            const double h1a = fmax(1e-6, h0 * 1e-3);
+            const double h1b = 0.3981071705534972 * ctr_math::inv_root10(fmax(d1sq, d2sq));
+            const double h1 = (d1sq <= 1e-30 && d2sq <= 1e-30) ? h1a : h1b;
+            ha = fmin(fmin(100.0 * h0, h1), interval);
+            t = t0;
+            need_init = false;
+            new_step = true;
+        }
+        {
+            const double ms = 10.0 * ctr_math::gap_up(t);
+            min_step = new_step ? ms : min_step;
+            ha = (new_step && ha < ms) ? ms : ha;
+            rejected = new_step ? false : rejected;
+            new_step = false;
+        }
+        if (!(ha >= min_step)) {
+            if (ha < min_step) {
+                st.status |= CTR_STATUS_STEP_UNDERFLOW;
+            } else {
+                rA = rB = NAN;
+                st.status |= CTR_STATUS_NAN;
+            }
+            break;
+        }
+        double tnew = t + ha;
+        if (tnew - tb > 0.0) tnew = tb;
+        const double h = tnew - t;
+        ha = fabs(h);
+        if (__ballot(lv3) == 0)
+            rk45_attempt_pair<2, CAREFUL>(p, m0, odd, A, B, U, V, rA, rB, fA, fB, fU, t, tb, ha, h, tnew, rejected,
+                                          new_step, need_init, st);
+        else
+            rk45_attempt_pair<3, CAREFUL>(p, m0, odd, A, B, U, V, rA, rB, fA, fB, fU, t, tb, ha, h, tnew, rejected,
+                                          new_step, need_init, st);
+    }
+    tip[0] = dpp_qp<DPP_FROM_EVEN>(rA);
+    tip[1] = dpp_qp<DPP_FROM_EVEN>(rB);
+    tip[2] = dpp_qp<DPP_FROM_ODD>(rA);
+    if (isnan(tip[0]) || isnan(tip[1]) || isnan(tip[2])) st.status |= CTR_STATUS_NAN;
+}
+
+// ------------------------------------------------------------------------------------------
 // Env logic
 // ------------------------------------------------------------------------------------------
 // obs.py:166-183 in float32 with numpy-2 scalar rules (python float -> float32).

@@ -985,8 +985,14 @@ __device__ __forceinline__ void step_body(const KCfg &kc, const ctr_batch_t &b, 
 #ifndef CTR_RK4_PAIR
 #define CTR_RK4_PAIR 1
 #endif
+// The headline (MODE 0, scipy RK45) on lane pairs (fk_pair_rk45): an A/B experiment, off in the
+// product build.  Measured 92.5-95.5 us against 72.3 us one env per lane (VERDICT r5 item 4,
+// DESIGN.md 3 "RK45 on lane pairs", profiles/r06_rk45pair_ab.txt); built by tools/experiments/ab_rk45pair.sh.
+#ifndef CTR_RK45_PAIR
+#define CTR_RK45_PAIR 0
+#endif
 template <int MODE>
-constexpr bool pair_mode() { return CTR_RK4_PAIR && MODE == 2; }
+constexpr bool pair_mode() { return (CTR_RK4_PAIR && MODE == 2) || (CTR_RK45_PAIR && MODE == 0); }
 template <int MODE>
 constexpr int step_block() { return pair_mode<MODE>() ? 2 * BLOCK : BLOCK; }
 template <int MODE>
@@ -1003,7 +1009,24 @@ __device__ __forceinline__ int pair_work_bucket(const ctr_system_t &sy, const fl
     return 255 - (int)fmin(fmax(w * 255.0, 0.0), 255.0);
 }
 
-template <bool HER>
+// scipy RK45 (the CTR_RK45_PAIR experiment): the attempts follow the segment count (each gap
+// restarts the solver), so the key is the number of segment ends beyond s = 0 (the tubes'
+// curvature starts and tips: correlation 0.88 with the oracle's RHS count, the extension key
+// alone 0.68), the extension key breaking ties
+__device__ __forceinline__ int pair_work_bucket_rk45(const ctr_system_t &sy, const float q[6], double inv_wmax)
+{
+    int nsa = 0;
+    #pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double tipi = (double)q[i] + sy.L[i];
+        nsa += (tipi > 0.0) + (tipi - sy.Lc[i] > 0.0);
+    }
+    const int ext = 255 - pair_work_bucket(sy, q, inv_wmax);                   // 0 .. 255
+    const double w = ((double)nsa + 0.9 * (double)ext * (1.0 / 255.0)) * (1.0 / 7.0);
+    return 255 - (int)fmin(fmax(w * 255.0, 0.0), 255.0);
+}
+
+template <int MODE, bool HER>
 __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t &b, const float *__restrict__ actions,
                                                const ctr_step_out_t &o, int32_t autoreset, const HerK &hk)
 {
@@ -1047,7 +1070,12 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     // its bucket (in atomic order: the deal, not any result, depends on it) -- then its prefix sums
     double lmax = 0.0;
     for (int k = 0; k < kc.c.n_systems; ++k) lmax = fmax(lmax, s_sys[k].L[1]);
+#if defined(CTR_RK45_KEY_NSEG)
+    const int bkt = !in_n ? 255 : MODE == 0 ? pair_work_bucket_rk45(s_sys[sn], q, 1.0 / (4.0 * lmax))
+                                            : pair_work_bucket(s_sys[sn], q, 1.0 / (4.0 * lmax));
+#else
     const int bkt = in_n ? pair_work_bucket(s_sys[sn], q, 1.0 / (4.0 * lmax)) : 255;
+#endif
     int place = 0;
     if (!odd) {
         place = atomicAdd(&s_hist[bkt], 1);
@@ -1096,13 +1124,18 @@ __device__ __forceinline__ void step_body_pair(const KCfg &kc, const ctr_batch_t
     float4 grow = make_float4(0.f, 0.f, 0.f, 0.f);
     PoolPre pp;
     // the time-limit resets' rows in flight during the FK (the others load theirs when done)
-    if (in && j == (HER ? 0 : 1)) pool_prefetch(kc, b, e, autoreset, pp, t_in, ep_in);
+    if (MODE != 0 && in && j == (HER ? 0 : 1)) pool_prefetch(kc, b, e, autoreset, pp, t_in, ep_in);
     const SysK &sy = in ? episode_sys_at(kc, s_sys, s_raw, s, ep_in, (uint64_t)(b.env_base + e), pr) : s_sys[0];
     const double qd[6] = {(double)q[0], (double)q[1], (double)q[2], (double)q[3], (double)q[4], (double)q[5]};
     FkStats st = {0, 0, 0, 0, 0};
     double ag[3];
-    if (fk_needs_careful_trig(qd)) fk_pair_rk4<true>(sy, qd, odd, ag, st, (double)kc.c.rk4_steps_per_m);
-    else fk_pair_rk4<false>(sy, qd, odd, ag, st, (double)kc.c.rk4_steps_per_m);
+    if constexpr (MODE == 0) {
+        if (fk_needs_careful_trig(qd)) fk_pair_rk45<true>(sy, qd, odd, ag, st);
+        else fk_pair_rk45<false>(sy, qd, odd, ag, st);
+    } else {
+        if (fk_needs_careful_trig(qd)) fk_pair_rk4<true>(sy, qd, odd, ag, st, (double)kc.c.rk4_steps_per_m);
+        else fk_pair_rk4<false>(sy, qd, odd, ag, st, (double)kc.c.rk4_steps_per_m);
+    }
     if constexpr (HER) {
         if (live) {
             double dg_in[3];
@@ -1120,7 +1153,7 @@ template <int MODE>
 __global__ __launch_bounds__(step_block<MODE>()) void k_step(KCfg kc, ctr_batch_t b, const float *__restrict__ actions,
                                                                 ctr_step_out_t o, int32_t autoreset)
 {
-    if constexpr (pair_mode<MODE>()) step_body_pair<false>(kc, b, actions, o, autoreset, HerK{});
+    if constexpr (pair_mode<MODE>()) step_body_pair<MODE, false>(kc, b, actions, o, autoreset, HerK{});
     else step_body<MODE, false>(kc, b, actions, o, autoreset, HerK{});
 }
 
@@ -1129,7 +1162,7 @@ __global__ __launch_bounds__(step_block<MODE>()) void k_step_her(KCfg kc, ctr_ba
                                                                     const float *__restrict__ actions,
                                                                     ctr_step_out_t o, int32_t autoreset, HerK hk)
 {
-    if constexpr (pair_mode<MODE>()) step_body_pair<true>(kc, b, actions, o, autoreset, hk);
+    if constexpr (pair_mode<MODE>()) step_body_pair<MODE, true>(kc, b, actions, o, autoreset, hk);
     else step_body<MODE, true>(kc, b, actions, o, autoreset, hk);
 }
 
@@ -1864,11 +1897,16 @@ int step_launch(const ctr_env_config_t *cfg, const ctr_batch_t *batch, const flo
     HerK hk = {};
     if (her) hk.h = *her;
     const int32_t her_on = her != nullptr;
-    if (kc.mode == 2 && pair_mode<2>()) {
-        // configs[4]: 256 envs per 512-lane workgroup (k_step_pair); dynamic LDS: one domain table per env
-        const dim3 g((unsigned)((b.n + BLOCK - 1) / BLOCK)), blk(step_block<2>());
-        if (her) hipLaunchKernelGGL(k_step_her<2>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
-        else hipLaunchKernelGGL(k_step<2>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+    if ((kc.mode == 2 && pair_mode<2>()) || (kc.mode == 0 && pair_mode<0>())) {
+        // configs[4]: 256 envs per 512-lane workgroup (step_body_pair); dynamic LDS: one domain table per env
+        const dim3 g((unsigned)((b.n + BLOCK - 1) / BLOCK)), blk(2 * BLOCK);
+        if (kc.mode == 0) {
+            if (her) hipLaunchKernelGGL(k_step_her<0>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
+            else hipLaunchKernelGGL(k_step<0>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+        } else {
+            if (her) hipLaunchKernelGGL(k_step_her<2>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset, hk);
+            else hipLaunchKernelGGL(k_step<2>, g, blk, lane_lds_bytes(kc), s, kc, b, actions, o, autoreset);
+        }
     } else {
         const int64_t lanes = (kc.mode & 6) == 6 ? SEG_GROUP * b.n : b.n;      // k_step's lanes per env
         if (her)
